@@ -1,0 +1,208 @@
+/*
+ * revel_wal.h -- C-ABI drop-in boundary for Revel's write-ahead-log record
+ * path, MI355X-native (gfx950).
+ *
+ * Reference: guimingyue/revel @ v0.  Each entry point names the reference
+ * interface it replaces (file:line).  The reference is a Rust crate whose
+ * WAL surface is crate-internal (lib.rs:24,33-38), so the binding a Revel
+ * maintainer adds is the `extern "C"` block shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no C++ or torch types.
+ *  - Status codes mirror `enum Error` (src/error.rs:16-23); 0 = Ok.
+ *  - The caller owns every buffer it passes.  Opaque handles are owned by the
+ *    caller after *_new and released with the matching *_free.
+ *  - Handles are single-threaded, like the reference's Rc<RefCell<..>> types
+ *    (log_writer.rs:26, log_reader.rs:44-56).  Use one writer/reader/GPU
+ *    context per thread; distinct handles may be used concurrently.
+ *  - Every GPU entry point fails loudly (REVEL_NOT_SUPPORT) when no gfx950
+ *    device is present; there is no CPU fallback behind them.
+ */
+#ifndef REVEL_WAL_H_
+#define REVEL_WAL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: src/error.rs:16-23 ---------------------------------- */
+#define REVEL_OK 0
+#define REVEL_NOT_FOUND 1
+#define REVEL_CORRUPTION 2
+#define REVEL_NOT_SUPPORT 3
+#define REVEL_INVALID_ARGUMENT 4
+#define REVEL_IO_ERROR 5
+
+/* ---- on-disk format: src/log_format.rs:14-30 --------------------------- */
+#define REVEL_BLOCK_SIZE 32768
+#define REVEL_HEADER_SIZE 7
+#define REVEL_ZERO_TYPE 0
+#define REVEL_FULL_TYPE 1
+#define REVEL_FIRST_TYPE 2
+#define REVEL_MIDDLE_TYPE 3
+#define REVEL_LAST_TYPE 4
+#define REVEL_MAX_RECORD_TYPE 4
+/* Payload bytes of a FULL record that fills one block exactly. */
+#define REVEL_FULL_BLOCK_PAYLOAD (REVEL_BLOCK_SIZE - REVEL_HEADER_SIZE)
+
+/* ---- CRC32C: src/util/crc.rs ------------------------------------------- */
+/* crc.rs:17-19  `pub fn value(data: &[u8]) -> u32` */
+uint32_t revel_crc32c_value(const uint8_t* data, size_t n);
+/* crc.rs:22-27  `pub fn extend(init: u8, data: &[u8]) -> u32` -- CRC of the
+ * single byte `init` followed by data (init is a prefix byte, NOT a crc). */
+uint32_t revel_crc32c_extend(uint8_t init, const uint8_t* data, size_t n);
+/* crc.rs:36-38  `pub const fn mask(crc: u32) -> u32` */
+uint32_t revel_crc32c_mask(uint32_t crc);
+/* crc.rs:41-44  `pub const fn unmask(masked_crc: u32) -> u32` */
+uint32_t revel_crc32c_unmask(uint32_t masked_crc);
+
+/* ---- files: src/env.rs -------------------------------------------------- */
+typedef struct revel_writable_file revel_writable_file;
+typedef struct revel_sequential_file revel_sequential_file;
+
+/* env.rs:201-230 `MemoryWritableFile::new(Vec::new())` */
+revel_writable_file* revel_memory_writable_file_new(void);
+/* env.rs:25-38 `new_writable_file(filename)` (truncate|create|write). */
+int revel_posix_writable_file_new(const char* path, revel_writable_file** out);
+/* env.rs:40-50 `trait WritableFile { append, flush, close, sync }` */
+int revel_writable_file_append(revel_writable_file* f, const uint8_t* data, size_t n);
+int revel_writable_file_flush(revel_writable_file* f);
+int revel_writable_file_close(revel_writable_file* f);
+int revel_writable_file_sync(revel_writable_file* f);
+/* Accessor the reference lacks (env.rs:201-204 keeps `memory` private):
+ * borrow the bytes of a memory file; valid until the next append/free.
+ * REVEL_INVALID_ARGUMENT for a posix file. */
+int revel_memory_writable_file_contents(const revel_writable_file* f, const uint8_t** data, size_t* n);
+void revel_writable_file_free(revel_writable_file* f);
+
+/* env.rs:232-246 `MemorySequentialFile::new(Rc<Vec<u8>>)` -- copies data. */
+revel_sequential_file* revel_memory_sequential_file_new(const uint8_t* data, size_t n);
+/* Posix sequential file.  The reference declares PosixSequentialFile
+ * (env.rs:153-175) but gives it no constructor. */
+int revel_posix_sequential_file_new(const char* path, revel_sequential_file** out);
+/* env.rs:52-57 `fn read(&self, scratch) -> Result<Slice>`: fills up to n
+ * bytes of scratch, *got = bytes filled (0 at EOF). */
+int revel_sequential_file_read(revel_sequential_file* f, uint8_t* scratch, size_t n, size_t* got);
+/* env.rs:56 `fn skip(&self, n)`: RELATIVE skip for both kinds (the
+ * reference's Posix impl seeks absolute, env.rs:171-174: App. A #6). */
+int revel_sequential_file_skip(revel_sequential_file* f, uint64_t n);
+void revel_sequential_file_free(revel_sequential_file* f);
+
+/* ---- log writer: src/log_writer.rs -------------------------------------- */
+typedef struct revel_log_writer revel_log_writer;
+/* log_writer.rs:41-53 `Writer::new(dest)` / `new_with_block_offset(dest, off)`.
+ * The writer borrows `dest` (the reference shares it via Rc, db.rs:56-63);
+ * dest must outlive the writer.  block_offset is taken as given. */
+revel_log_writer* revel_log_writer_new(revel_writable_file* dest, uint64_t block_offset);
+/* log_writer.rs:58-97 `add_record(&mut self, slice) -> Result<()>`:
+ * fragments into FULL/FIRST/MIDDLE/LAST physical records, zero-pads block
+ * trailers < 7 bytes, header = [mask(crc32c(type||payload)) LE][len LE16][type],
+ * flushes after every physical record (log_writer.rs:119). */
+int revel_log_writer_add_record(revel_log_writer* w, const uint8_t* data, size_t n);
+uint64_t revel_log_writer_block_offset(const revel_log_writer* w);
+void revel_log_writer_free(revel_log_writer* w);
+
+/* ---- GPU context -------------------------------------------------------- */
+typedef struct revel_gpu_context revel_gpu_context;
+/* Number of visible gfx950 devices (0 on a host without one). */
+int revel_gpu_device_count(int* count);
+/* One context per (thread, device): owns a HIP stream and scratch. */
+int revel_gpu_context_new(int device, revel_gpu_context** out);
+void revel_gpu_context_free(revel_gpu_context* ctx);
+/* The context's stream as an opaque hipStream_t. */
+void* revel_gpu_context_stream(revel_gpu_context* ctx);
+
+/* ---- log reader: src/log_reader.rs ------------------------------------- */
+typedef struct revel_log_reader revel_log_reader;
+/* log_reader.rs:62-74 `Reader::new(file, checksum, initial_offset)`.
+ * The reader takes ownership of `file` (Box<dyn SequentialFile>).
+ * With checksum != 0 every physical record's CRC is verified ON THE GPU of
+ * `gpu` (required: REVEL_NOT_SUPPORT if NULL); with checksum == 0, gpu may
+ * be NULL.  `window_bytes` = bytes read + verified per GPU batch (rounded
+ * up to a block multiple; 0 = default 64 MiB). */
+int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t initial_offset,
+                         revel_gpu_context* gpu, size_t window_bytes, revel_log_reader** out);
+/* log_reader.rs:76-153 `read_record(&mut self, scratch) -> Result<Slice>`.
+ * The returned bytes (data, n) borrow reader-owned memory valid until the next call (the
+ * reference borrows the caller's scratch).  EOF: REVEL_OK with *n == 0 and
+ * *data == NULL (the reference returns an empty Slice, :140).  A checksum
+ * mismatch returns REVEL_IO_ERROR, as the reference does (:142-152). */
+int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size_t* n);
+/* File offset of the first physical record of the last returned record. */
+uint64_t revel_log_reader_last_record_offset(const revel_log_reader* r);
+void revel_log_reader_free(revel_log_reader* r);
+
+/* ---- device-resident CRC engine (the hot path) ------------------------- */
+/* Per physical record result of revel_gpu_verify_records (24 bytes). */
+typedef struct revel_record_result {
+    uint64_t file_offset;   /* offset of the 7-byte header (base_offset + in-image offset) */
+    uint32_t length;        /* payload length from the header */
+    uint32_t stored_crc;    /* masked CRC stored in the header (coding.rs:139-144) */
+    uint32_t computed_crc;  /* mask(crc32c(type || payload[:length])) */
+    uint8_t type;           /* record type byte */
+    uint8_t status;         /* REVEL_REC_* */
+    uint8_t reserved[2];
+} revel_record_result;
+
+#define REVEL_REC_OK 0
+#define REVEL_REC_BAD_CHECKSUM 1
+#define REVEL_REC_BAD_LENGTH 2   /* 7 + length runs past the block end */
+#define REVEL_REC_ZERO 3         /* type 0, length 0: preallocated region (log_reader.rs:195-198) */
+
+/* Config C2 kernel.  d_blocks: nblocks * 32768 device bytes, every block one
+ * FULL record of 32761 bytes.  d_masked_out[b] = mask(crc32c(block[6:32768]))
+ * = the value log_writer.rs:107-111 stores for that payload;
+ * d_ok[b] = (stored == computed && length == 32761 && type == FULL).
+ * d_ok may be NULL.  Asynchronous on `stream` (NULL = context stream). */
+int revel_gpu_crc_full_blocks(revel_gpu_context* ctx, const void* d_blocks, size_t nblocks,
+                              uint32_t* d_masked_out, uint8_t* d_ok, void* stream);
+
+/* GPU append framing for config C2 (log_writer.rs:99-124 on device): given
+ * nblocks * 32768 bytes whose payload bytes [7:32768) are filled, write each
+ * block's FULL header [mask(crc) LE][0xF9 0x7F][0x01] in place. */
+int revel_gpu_frame_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t nblocks, void* stream);
+
+/* Variable-layout verify (config C3).  Two steps so the caller sizes the
+ * output:  (1) count physical records of each block of the image
+ * (d_counts[nblocks]); (2) walk + CRC every record, writing record k of
+ * block b to d_out[d_first[b] + k] where d_first is the exclusive prefix sum
+ * of d_counts (revel_gpu_exclusive_scan_u32 computes it on device).
+ * nbytes need not be a block multiple (the last block may be partial). */
+int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,
+                            uint32_t* d_counts, void* stream);
+int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, uint32_t* d_out,
+                                 size_t n, void* stream);
+int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,
+                             uint64_t base_offset, const uint32_t* d_first,
+                             revel_record_result* d_out, void* stream);
+
+/* ---- device plumbing (used by the reader, tests and bench) -------------- */
+int revel_gpu_malloc(revel_gpu_context* ctx, size_t n, void** d_ptr);
+int revel_gpu_free(revel_gpu_context* ctx, void* d_ptr);
+int revel_gpu_host_alloc(revel_gpu_context* ctx, size_t n, void** h_pinned);
+int revel_gpu_host_free(revel_gpu_context* ctx, void* h_pinned);
+int revel_gpu_memcpy_h2d(revel_gpu_context* ctx, void* d_dst, const void* h_src, size_t n, void* stream);
+int revel_gpu_memcpy_d2h(revel_gpu_context* ctx, void* h_dst, const void* d_src, size_t n, void* stream);
+int revel_gpu_memset(revel_gpu_context* ctx, void* d_dst, int value, size_t n, void* stream);
+int revel_gpu_stream_synchronize(revel_gpu_context* ctx, void* stream);
+int revel_gpu_device_synchronize(revel_gpu_context* ctx);
+/* Fill nblocks full-type blocks on device: payload = splitmix64(seed ^ (first+b))
+ * (same bytes as oracle_synth_full_blocks), then frame the headers. */
+int revel_gpu_synth_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t nblocks,
+                                uint64_t seed, uint64_t first, void* stream);
+/* HIP events for timing on a stream. */
+int revel_gpu_event_new(revel_gpu_context* ctx, void** ev);
+int revel_gpu_event_record(revel_gpu_context* ctx, void* ev, void* stream);
+int revel_gpu_event_elapsed_ms(revel_gpu_context* ctx, void* start, void* stop, float* ms);
+int revel_gpu_event_free(revel_gpu_context* ctx, void* ev);
+/* Human-readable description of the last error on this thread. */
+const char* revel_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* REVEL_WAL_H_ */

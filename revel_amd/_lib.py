@@ -1,0 +1,125 @@
+"""ctypes binding of ``librevel_wal.so`` (the C-ABI in include/revel_wal.h).
+
+The library is built in-tree (``make -C revel_amd/csrc``, or
+``__graft_entry__.build()``).  Loading fails loudly if it is missing: there
+is no Python or CPU fallback for anything behind it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_float, c_int, c_size_t, c_uint8, c_uint32,
+                    c_uint64, c_void_p)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librevel_wal.so")
+
+# status codes: src/error.rs:16-23
+OK, NOT_FOUND, CORRUPTION, NOT_SUPPORT, INVALID_ARGUMENT, IO_ERROR = 0, 1, 2, 3, 4, 5
+ERROR_NAMES = {1: "NotFound", 2: "Corruption", 3: "NotSupport", 4: "InvalidArgument", 5: "IOError"}
+
+BLOCK_SIZE = 32768
+HEADER_SIZE = 7
+ZERO_TYPE, FULL_TYPE, FIRST_TYPE, MIDDLE_TYPE, LAST_TYPE = 0, 1, 2, 3, 4
+REC_OK, REC_BAD_CHECKSUM, REC_BAD_LENGTH, REC_ZERO = 0, 1, 2, 3
+
+
+class RecordResult(Structure):
+    _fields_ = [("file_offset", c_uint64), ("length", c_uint32), ("stored_crc", c_uint32),
+                ("computed_crc", c_uint32), ("type", c_uint8), ("status", c_uint8),
+                ("reserved", c_uint8 * 2)]
+
+
+assert ctypes.sizeof(RecordResult) == 24
+
+# name -> (restype, argtypes); every symbol declared in include/revel_wal.h
+SIGNATURES = {
+    "revel_crc32c_value": (c_uint32, [c_void_p, c_size_t]),
+    "revel_crc32c_extend": (c_uint32, [c_uint8, c_void_p, c_size_t]),
+    "revel_crc32c_mask": (c_uint32, [c_uint32]),
+    "revel_crc32c_unmask": (c_uint32, [c_uint32]),
+    "revel_memory_writable_file_new": (c_void_p, []),
+    "revel_posix_writable_file_new": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "revel_writable_file_append": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "revel_writable_file_flush": (c_int, [c_void_p]),
+    "revel_writable_file_close": (c_int, [c_void_p]),
+    "revel_writable_file_sync": (c_int, [c_void_p]),
+    "revel_memory_writable_file_contents": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
+    "revel_writable_file_free": (None, [c_void_p]),
+    "revel_memory_sequential_file_new": (c_void_p, [c_void_p, c_size_t]),
+    "revel_posix_sequential_file_new": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "revel_sequential_file_read": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_size_t)]),
+    "revel_sequential_file_skip": (c_int, [c_void_p, c_uint64]),
+    "revel_sequential_file_free": (None, [c_void_p]),
+    "revel_log_writer_new": (c_void_p, [c_void_p, c_uint64]),
+    "revel_log_writer_add_record": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "revel_log_writer_block_offset": (c_uint64, [c_void_p]),
+    "revel_log_writer_free": (None, [c_void_p]),
+    "revel_gpu_device_count": (c_int, [POINTER(c_int)]),
+    "revel_gpu_context_new": (c_int, [c_int, POINTER(c_void_p)]),
+    "revel_gpu_context_free": (None, [c_void_p]),
+    "revel_gpu_context_stream": (c_void_p, [c_void_p]),
+    "revel_log_reader_new": (c_int, [c_void_p, c_int, c_uint64, c_void_p, c_size_t, POINTER(c_void_p)]),
+    "revel_log_reader_read_record": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
+    "revel_log_reader_last_record_offset": (c_uint64, [c_void_p]),
+    "revel_log_reader_free": (None, [c_void_p]),
+    "revel_gpu_crc_full_blocks": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+    "revel_gpu_frame_full_blocks": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "revel_gpu_count_records": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
+    "revel_gpu_exclusive_scan_u32": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "revel_gpu_verify_records": (c_int, [c_void_p, c_void_p, c_size_t, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "revel_gpu_malloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "revel_gpu_free": (c_int, [c_void_p, c_void_p]),
+    "revel_gpu_host_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "revel_gpu_host_free": (c_int, [c_void_p, c_void_p]),
+    "revel_gpu_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "revel_gpu_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "revel_gpu_memset": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_void_p]),
+    "revel_gpu_stream_synchronize": (c_int, [c_void_p, c_void_p]),
+    "revel_gpu_device_synchronize": (c_int, [c_void_p]),
+    "revel_gpu_synth_full_blocks": (c_int, [c_void_p, c_void_p, c_size_t, c_uint64, c_uint64, c_void_p]),
+    "revel_gpu_event_new": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "revel_gpu_event_record": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "revel_gpu_event_elapsed_ms": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_float)]),
+    "revel_gpu_event_free": (c_int, [c_void_p, c_void_p]),
+    "revel_last_error": (c_char_p, []),
+}
+
+# exported experiment hooks (not part of the public header)
+EXTRA_SIGNATURES = {
+    "revel_gpu_crc_full_blocks_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p,
+                                                  c_void_p]),
+}
+
+_lib = None
+
+
+class RevelError(RuntimeError):
+    """A non-zero status from the C-ABI (codes of src/error.rs:16-23)."""
+
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        name = ERROR_NAMES.get(code, f"status {code}")
+        super().__init__(f"{name}: {what}" if what else name)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `make -C revel_amd/csrc` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (there is no fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in {**SIGNATURES, **EXTRA_SIGNATURES}.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != OK:
+        msg = lib().revel_last_error()
+        raise RevelError(rc, msg.decode() if msg else "")

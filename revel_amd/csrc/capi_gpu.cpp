@@ -1,0 +1,280 @@
+// capi_gpu.cpp -- extern "C" GPU entry points of include/revel_wal.h.
+// Every call validates its context and arguments, binds the context's device
+// on the calling thread and launches on the given stream (NULL = the
+// context's own).  There is no CPU fallback: without a gfx950 device every
+// entry point returns REVEL_NOT_SUPPORT.
+#include <hip/hip_runtime_api.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "gpu_internal.h"
+
+namespace revel {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+}  // namespace revel
+
+using revel::set_error;
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    return set_error(REVEL_IO_ERROR, "%s: %s", what, hipGetErrorString(e));
+}
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
+    return strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+struct Bind {
+    hipError_t err;
+    explicit Bind(const revel_gpu_context* c) : err(hipSetDevice(c->di.device)) {}
+};
+
+hipStream_t pick(const revel_gpu_context* c, void* stream) {
+    return stream ? static_cast<hipStream_t>(stream) : c->stream;
+}
+
+#define CHECK_CTX(ctx)                                                                        \
+    do {                                                                                      \
+        if (!(ctx)) return set_error(REVEL_INVALID_ARGUMENT, "null revel_gpu_context");     \
+        Bind bind_(ctx);                                                                      \
+        if (bind_.err != hipSuccess) return hip_fail(bind_.err, "hipSetDevice");             \
+    } while (0)
+
+#define HIP_TRY(expr, what)                          \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return hip_fail(e_, what); \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+const char* revel_last_error(void) { return revel::g_last_error.c_str(); }
+
+int revel_gpu_device_count(int* count) {
+    if (!count) return set_error(REVEL_INVALID_ARGUMENT, "null count");
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return REVEL_OK;
+    }
+    int k = 0;
+    for (int d = 0; d < n; ++d) k += is_gfx950(d) ? 1 : 0;
+    *count = k;
+    return REVEL_OK;
+}
+
+int revel_gpu_context_new(int device, revel_gpu_context** out) {
+    if (!out) return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return set_error(REVEL_NOT_SUPPORT, "no HIP device visible: the CRC engine needs a gfx950 GPU");
+    }
+    if (device < 0 || device >= n) return set_error(REVEL_INVALID_ARGUMENT, "device %d out of range (0..%d)", device, n - 1);
+    if (!is_gfx950(device)) return set_error(REVEL_NOT_SUPPORT, "device %d is not gfx950", device);
+    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    auto* c = new revel_gpu_context;
+    c->di.device = device;
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->di.num_cu = cu;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    *out = c;
+    return REVEL_OK;
+}
+
+void revel_gpu_context_free(revel_gpu_context* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->di.device);
+    if (ctx->stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+void* revel_gpu_context_stream(revel_gpu_context* ctx) { return ctx ? ctx->stream : nullptr; }
+
+int revel_gpu_crc_full_blocks(revel_gpu_context* ctx, const void* d_blocks, size_t nblocks, uint32_t* d_masked_out,
+                              uint8_t* d_ok, void* stream) {
+    CHECK_CTX(ctx);
+    if (nblocks == 0) return REVEL_OK;
+    if (!d_blocks || !d_masked_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::crc_full_blocks_variant(ctx->di, 0, d_blocks, nblocks, d_masked_out, d_ok, pick(ctx, stream)),
+            "crc_full_blocks launch");
+    return REVEL_OK;
+}
+
+// Experiment hook (not in the public header): same contract as
+// revel_gpu_crc_full_blocks for a given kernel variant.
+int revel_gpu_crc_full_blocks_variant(revel_gpu_context* ctx, int variant, const void* d_blocks, size_t nblocks,
+                                      uint32_t* d_masked_out, uint8_t* d_ok, void* stream) {
+    CHECK_CTX(ctx);
+    if (nblocks == 0) return REVEL_OK;
+    if (!d_blocks || !d_masked_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::crc_full_blocks_variant(ctx->di, variant, d_blocks, nblocks, d_masked_out, d_ok, pick(ctx, stream)),
+            "crc_full_blocks_variant launch");
+    return REVEL_OK;
+}
+
+int revel_gpu_frame_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t nblocks, void* stream) {
+    CHECK_CTX(ctx);
+    if (nblocks == 0) return REVEL_OK;
+    if (!d_blocks) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::frame_full_blocks(ctx->di, d_blocks, nblocks, pick(ctx, stream)), "frame_full_blocks launch");
+    return REVEL_OK;
+}
+
+int revel_gpu_synth_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t nblocks, uint64_t seed, uint64_t first,
+                                void* stream) {
+    CHECK_CTX(ctx);
+    if (nblocks == 0) return REVEL_OK;
+    if (!d_blocks) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::synth_full_blocks(ctx->di, d_blocks, nblocks, seed, first, pick(ctx, stream)), "synth launch");
+    return REVEL_OK;
+}
+
+int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts,
+                            void* stream) {
+    CHECK_CTX(ctx);
+    if (nbytes == 0) return REVEL_OK;
+    if (!d_image || !d_counts) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, pick(ctx, stream)), "count_records launch");
+    return REVEL_OK;
+}
+
+int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                 void* stream) {
+    CHECK_CTX(ctx);
+    if (n == 0) return REVEL_OK;
+    if (!d_in || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::exclusive_scan_u32(ctx->di, d_in, d_out, n, pick(ctx, stream)), "scan launch");
+    return REVEL_OK;
+}
+
+int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint64_t base_offset,
+                             const uint32_t* d_first, revel_record_result* d_out, void* stream) {
+    CHECK_CTX(ctx);
+    if (nbytes == 0) return REVEL_OK;
+    if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::verify_records(ctx->di, d_image, nbytes, base_offset, d_first, d_out, pick(ctx, stream)),
+            "verify_records launch");
+    return REVEL_OK;
+}
+
+int revel_gpu_malloc(revel_gpu_context* ctx, size_t n, void** d_ptr) {
+    CHECK_CTX(ctx);
+    if (!d_ptr) return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    *d_ptr = nullptr;
+    HIP_TRY(hipMalloc(d_ptr, n ? n : 1), "hipMalloc");
+    return REVEL_OK;
+}
+
+int revel_gpu_free(revel_gpu_context* ctx, void* d_ptr) {
+    CHECK_CTX(ctx);
+    if (d_ptr) HIP_TRY(hipFree(d_ptr), "hipFree");
+    return REVEL_OK;
+}
+
+int revel_gpu_host_alloc(revel_gpu_context* ctx, size_t n, void** h) {
+    CHECK_CTX(ctx);
+    if (!h) return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    *h = nullptr;
+    HIP_TRY(hipHostMalloc(h, n ? n : 1, hipHostMallocDefault), "hipHostMalloc");
+    return REVEL_OK;
+}
+
+int revel_gpu_host_free(revel_gpu_context* ctx, void* h) {
+    CHECK_CTX(ctx);
+    if (h) HIP_TRY(hipHostFree(h), "hipHostFree");
+    return REVEL_OK;
+}
+
+int revel_gpu_memcpy_h2d(revel_gpu_context* ctx, void* d_dst, const void* h_src, size_t n, void* stream) {
+    CHECK_CTX(ctx);
+    if (n == 0) return REVEL_OK;
+    HIP_TRY(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, pick(ctx, stream)), "hipMemcpyAsync H2D");
+    return REVEL_OK;
+}
+
+int revel_gpu_memcpy_d2h(revel_gpu_context* ctx, void* h_dst, const void* d_src, size_t n, void* stream) {
+    CHECK_CTX(ctx);
+    if (n == 0) return REVEL_OK;
+    HIP_TRY(hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, pick(ctx, stream)), "hipMemcpyAsync D2H");
+    return REVEL_OK;
+}
+
+int revel_gpu_memset(revel_gpu_context* ctx, void* d_dst, int value, size_t n, void* stream) {
+    CHECK_CTX(ctx);
+    if (n == 0) return REVEL_OK;
+    HIP_TRY(hipMemsetAsync(d_dst, value, n, pick(ctx, stream)), "hipMemsetAsync");
+    return REVEL_OK;
+}
+
+int revel_gpu_stream_synchronize(revel_gpu_context* ctx, void* stream) {
+    CHECK_CTX(ctx);
+    HIP_TRY(hipStreamSynchronize(pick(ctx, stream)), "hipStreamSynchronize");
+    return REVEL_OK;
+}
+
+int revel_gpu_device_synchronize(revel_gpu_context* ctx) {
+    CHECK_CTX(ctx);
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    return REVEL_OK;
+}
+
+int revel_gpu_event_new(revel_gpu_context* ctx, void** ev) {
+    CHECK_CTX(ctx);
+    if (!ev) return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+    *ev = e;
+    return REVEL_OK;
+}
+
+int revel_gpu_event_record(revel_gpu_context* ctx, void* ev, void* stream) {
+    CHECK_CTX(ctx);
+    HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(ev), pick(ctx, stream)), "hipEventRecord");
+    return REVEL_OK;
+}
+
+int revel_gpu_event_elapsed_ms(revel_gpu_context* ctx, void* start, void* stop, float* ms) {
+    CHECK_CTX(ctx);
+    HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(stop)), "hipEventSynchronize");
+    HIP_TRY(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)),
+            "hipEventElapsedTime");
+    return REVEL_OK;
+}
+
+int revel_gpu_event_free(revel_gpu_context* ctx, void* ev) {
+    CHECK_CTX(ctx);
+    if (ev) HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(ev)), "hipEventDestroy");
+    return REVEL_OK;
+}
+
+}  // extern "C"

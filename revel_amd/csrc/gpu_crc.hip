@@ -1,0 +1,676 @@
+// gpu_crc.hip -- CDNA4 (gfx950) CRC-32C engine for Revel's WAL record path.
+//
+// Hot path (reference guimingyue/revel @ v0):
+//   log_writer.rs:107-111  crc = mask(extend(type, payload))  (writer side)
+//   log_reader.rs:200-206  unmask(stored) == value(type||payload) (reader side)
+//   util/crc.rs:13-44      CRC_32_ISCSI + mask/unmask
+//
+// Work decomposition: ONE WAVEFRONT PER 32 KiB LOG BLOCK.  Lane i owns the
+// contiguous 512-byte chunk [512 i, 512 i + 512) of its block and runs a
+// table-driven CRC over it from a zero register; the 64 partial registers are
+// then combined by a wavefront GF(2) polynomial-shift reduction:
+//     R(block) = XOR_i  R_i * x^(8*512*(63-i))  mod P
+// (each lane multiplies by its own constant, then an xor-butterfly across the
+// wave).  Init/xorout enter once per record as a length-dependent constant.
+// No MFMA: this is GF(2) arithmetic, not a contraction.
+//
+// Lookup tables live in LDS, replicated 32x so that lane (l & 31) always hits
+// bank (l & 31) for ds_read_b32: bank-conflict-free gathers whatever the data.
+// The LDS byte address of entry e for lane l is (e << 8) | ((l & 31) << 2)
+// | (region << 16), built by ONE v_perm_b32 per lookup.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "crc32c_math.h"
+#include "gpu_internal.h"
+
+using namespace revel;
+
+namespace {
+
+constexpr SliceTables kTables = make_slice_tables();
+
+// ---------------------------------------------------------------------------
+// Compile-time GF(2) constants
+// ---------------------------------------------------------------------------
+struct LaneShiftConsts {
+    uint32_t c[64];  // x^(8*512*(63-i)) mod P
+};
+constexpr LaneShiftConsts make_lane_shift() {
+    LaneShiftConsts s{};
+    for (int i = 0; i < 64; ++i) s.c[i] = x8n(512ull * (63 - i));
+    return s;
+}
+// x^(8*512*m) for m = 0..64 and x^(8*d) for d = 0..512: any shift inside a
+// block is one multmodp of two table entries.
+struct ShiftTables {
+    uint32_t chunk[65];
+    uint32_t byte[513];
+};
+constexpr ShiftTables make_shift_tables() {
+    ShiftTables s{};
+    for (int m = 0; m <= 64; ++m) s.chunk[m] = x8n(512ull * m);
+    uint32_t v = 0x80000000u;  // x^0
+    const uint32_t x8 = x8n(1);
+    for (int d = 0; d <= 512; ++d) {
+        s.byte[d] = v;
+        v = multmodp(x8, v);
+    }
+    return s;
+}
+
+__constant__ SliceTables c_tables = kTables;
+__constant__ LaneShiftConsts c_lane_shift = make_lane_shift();
+__constant__ ShiftTables c_shift = make_shift_tables();
+
+constexpr uint32_t kFullInitXor = init_xor(kFullCrcLen);
+constexpr uint32_t kFullTypeByte = 1u;
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Branch-free a*b mod P (reflected).  v_bfe_i32 turns a bit into 0/-1.
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        uint32_t am = (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - k, 1);
+        p ^= b & am;
+        uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
+        b = (b >> 1) ^ (kPolyReflected & bm);
+    }
+    return p;
+}
+
+// x^(8n) mod P for 0 <= n <= 32768 from the two shift tables.
+__device__ __forceinline__ uint32_t gf_x8n_block(uint32_t n) {
+    uint32_t m = n >> 9, d = n & 511u;
+    uint32_t a = c_shift.chunk[m];
+    return d ? gf_mul(a, c_shift.byte[d]) : a;
+}
+
+__device__ __forceinline__ uint32_t xor_reduce_wave(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t bytewise_step(uint32_t s, uint32_t b) {
+    return c_tables.t[0][(s ^ b) & 0xffu] ^ (s >> 8);
+}
+
+// LDS byte-address load (ds_read_b32 with immediate offset).  The tables are
+// a static __shared__ array, so its base folds into the instruction.
+template <int OFF>
+__device__ __forceinline__ uint32_t ldsw(const uint32_t* tab, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr + OFF);
+}
+
+// v_perm_b32 selectors: result byte0 <- lanec byte0 (lane*4), byte1 <- x byte k,
+// byte2 <- lanec byte2 (table region), byte3 <- 0.
+template <int K>
+struct Sel {
+    static constexpr uint32_t v = 0x0C020000u | ((4u + K) << 8) | 0x00u;
+};
+
+// ---------------------------------------------------------------------------
+// Table modes
+// ---------------------------------------------------------------------------
+enum TableMode : int {
+    TM_S4R = 0,  // slice-by-4, 32x replicated, 128 KiB LDS
+    TM_S2R = 1,  // slice-by-2, 32x replicated, 64 KiB LDS
+    TM_S4 = 2,   // slice-by-4, unreplicated, 4 KiB LDS (bank conflicts)
+};
+
+template <int TM>
+struct TableCfg;
+template <>
+struct TableCfg<TM_S4R> {
+    static constexpr uint32_t bytes = 131072;
+};
+template <>
+struct TableCfg<TM_S2R> {
+    static constexpr uint32_t bytes = 65536;
+};
+template <>
+struct TableCfg<TM_S4> {
+    static constexpr uint32_t bytes = 4096;
+};
+
+// Fill the LDS image of the tables (cooperatively, whole workgroup).
+template <int TM>
+__device__ void fill_tables(uint32_t* tab) {
+    const uint32_t ndw = TableCfg<TM>::bytes / 4;
+    for (uint32_t d = threadIdx.x; d < ndw; d += blockDim.x) {
+        uint32_t v;
+        if constexpr (TM == TM_S4) {
+            // [T3 | T2 | T1 | T0], 256 entries each: byte k of x indexes T(3-k)
+            v = c_tables.t[3 - (d >> 8)][d & 255u];
+        } else if constexpr (TM == TM_S4R) {
+            // region r (16384 dw) -> row e (64 dw) -> half h (32 dw) -> copy c
+            uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
+            // byte0 -> T3 (r0 h0), byte1 -> T2 (r0 h1), byte2 -> T1 (r1 h0), byte3 -> T0 (r1 h1)
+            v = c_tables.t[3 - (r * 2 + h)][e];
+        } else {
+            // S2R: row e = [T1 x32 | T0 x32]
+            uint32_t e = (d >> 6) & 255u, h = (d >> 5) & 1u;
+            v = c_tables.t[1 - h][e];
+        }
+        tab[d] = v;
+    }
+}
+
+struct LaneConst {
+    uint32_t lc0, lc1;
+};
+
+__device__ __forceinline__ LaneConst make_lane_const() {
+    uint32_t c4 = (lane_id() & 31u) << 2;
+    return {c4, c4 | 0x10000u};
+}
+
+// Absorb one little-endian 32-bit word into the raw register.
+template <int TM>
+__device__ __forceinline__ uint32_t absorb(uint32_t crc, uint32_t w, LaneConst L, const uint32_t* tab) {
+    uint32_t x = crc ^ w;
+    if constexpr (TM == TM_S4R) {
+        uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
+        uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
+        uint32_t a2 = __builtin_amdgcn_perm(x, L.lc1, Sel<2>::v);
+        uint32_t a3 = __builtin_amdgcn_perm(x, L.lc1, Sel<3>::v);
+        return (ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1)) ^ (ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3));
+    } else if constexpr (TM == TM_S2R) {
+        uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
+        uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
+        uint32_t c = ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1) ^ (x >> 16);
+        uint32_t a2 = __builtin_amdgcn_perm(c, L.lc0, Sel<0>::v);
+        uint32_t a3 = __builtin_amdgcn_perm(c, L.lc0, Sel<1>::v);
+        return ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3) ^ (c >> 16);
+    } else {
+        return (tab[x & 0xffu] ^ tab[256 + ((x >> 8) & 0xffu)]) ^
+               (tab[512 + ((x >> 16) & 0xffu)] ^ tab[768 + (x >> 24)]);
+    }
+}
+
+template <int TM>
+__device__ __forceinline__ uint32_t absorb4(uint32_t crc, uint4 v, LaneConst L, const uint32_t* tab) {
+    crc = absorb<TM>(crc, v.x, L, tab);
+    crc = absorb<TM>(crc, v.y, L, tab);
+    crc = absorb<TM>(crc, v.z, L, tab);
+    crc = absorb<TM>(crc, v.w, L, tab);
+    return crc;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldg4(const uint4* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
+// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
+// Returns lane 0's first 16 bytes through *hdr.
+template <int TM>
+__device__ __forceinline__ uint32_t full_block_lane_crc(const uint8_t* blk, LaneConst L, const uint32_t* tab,
+                                                        uint4* hdr, bool force_type) {
+    const uint4* p = reinterpret_cast<const uint4*>(blk) + lane_id() * 32;
+    const bool l0 = lane_id() == 0;
+    uint32_t crc = 0;
+    // 4 batches of 128 B; batch k+1's loads are issued before batch k is
+    // absorbed (sched_barrier keeps the scheduler from sinking them).
+    uint4 cur[8], nxt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cur[j] = ldg4(p + j);
+#pragma unroll
+    for (int batch = 0; batch < 4; ++batch) {
+        if (batch < 3) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nxt[j] = ldg4(p + (batch + 1) * 8 + j);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (batch == 0) {
+            *hdr = cur[0];
+            cur[0].x = l0 ? 0u : cur[0].x;
+            uint32_t y = force_type ? ((cur[0].y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16)) : cur[0].y;
+            cur[0].y = l0 ? (y & 0xFFFF0000u) : cur[0].y;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) crc = absorb4<TM>(crc, cur[j], L, tab);
+        __builtin_amdgcn_sched_barrier(0);
+        if (batch < 3) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+        }
+    }
+    return crc;
+}
+
+// ---------------------------------------------------------------------------
+// Config C2: one FULL record per block.
+// ---------------------------------------------------------------------------
+template <int TM, int THREADS, bool FRAME>
+__global__ __launch_bounds__(THREADS) void k_full_blocks(const uint8_t* __restrict__ blocks, uint64_t nblocks,
+                                                         uint32_t* __restrict__ masked_out,
+                                                         uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
+    __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
+    fill_tables<TM>(tab);
+    __syncthreads();
+    const LaneConst L = make_lane_const();
+    const uint32_t my_shift = c_lane_shift.c[lane_id()];
+    const uint64_t waves_per_wg = THREADS / 64;
+    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+        const uint8_t* blk = blocks + b * kBlockSize;
+        uint4 hdr;
+        uint32_t r = full_block_lane_crc<TM>(blk, L, tab, &hdr, FRAME);
+        r = xor_reduce_wave(gf_mul(my_shift, r));
+        const uint32_t masked = mask(r ^ kFullInitXor);
+        if (lane_id() == 0) {
+            if constexpr (FRAME) {
+                // header [mask(crc) LE][len LE16][type]; byte 7 is payload.
+                uint2 h;
+                h.x = masked;
+                h.y = (hdr.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16) | kFullPayload;
+                *reinterpret_cast<uint2*>(frame_dst + b * kBlockSize) = h;
+            } else {
+                masked_out[b] = masked;
+                if (ok_out) {
+                    const bool ok = (hdr.x == masked) && ((hdr.y & 0xFFFFu) == kFullPayload) &&
+                                    (((hdr.y >> 16) & 0xFFu) == kFullTypeByte);
+                    ok_out[b] = ok ? 1 : 0;
+                }
+            }
+        }
+    }
+}
+
+// Read-only streaming ceiling with the same grid and block assignment:
+// coalesced 16 B/lane loads of the whole block, xor-folded, 4 B written.
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_stream_ceiling(const uint8_t* __restrict__ blocks, uint64_t nblocks,
+                                                            uint32_t* __restrict__ out) {
+    const uint64_t waves_per_wg = THREADS / 64;
+    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+        const uint4* p = reinterpret_cast<const uint4*>(blocks + b * kBlockSize) + lane_id();
+        uint4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            uint4 v = ldg4(p + k * 64);
+            acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+        }
+        uint32_t r = xor_reduce_wave(acc.x ^ acc.y ^ acc.z ^ acc.w);
+        if (lane_id() == 0) out[b] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic C2 payloads: block b = splitmix64(seed ^ (first + b)) words.
+// ---------------------------------------------------------------------------
+__global__ void k_synth(uint64_t* __restrict__ dst, uint64_t nblocks, uint64_t seed, uint64_t first) {
+    const uint64_t words_per_block = kBlockSize / 8;
+    const uint64_t total = nblocks * words_per_block;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = i / words_per_block, w = i % words_per_block;
+        uint64_t z = (seed ^ (first + b)) + (w + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        dst[i] = z ^ (z >> 31);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Config C3: variable records (FULL/FIRST/MIDDLE/LAST mixes, padding, zeros).
+// ---------------------------------------------------------------------------
+struct Hdr {
+    uint32_t stored, len, type;
+};
+
+// Bytes [off, off+7) of a block of length bl, never reading at or past bl
+// (the image end need not be 4-byte aligned or padded).
+__device__ __forceinline__ Hdr read_header(const uint8_t* base, uint32_t off, uint32_t bl) {
+    const uint32_t a0 = off & ~3u;
+    uint32_t w0, w1, w2 = 0;
+    if (a0 + 12u <= bl) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(base + a0);
+        w0 = w[0]; w1 = w[1]; w2 = w[2];
+    } else {
+        uint8_t t[12];
+        for (uint32_t k = 0; k < 12; ++k) t[k] = a0 + k < bl ? base[a0 + k] : 0;
+        memcpy(&w0, t, 4); memcpy(&w1, t + 4, 4); memcpy(&w2, t + 8, 4);
+    }
+    const uint32_t sh = (off & 3u) * 8u;
+    const uint64_t lo = (uint64_t(w1) << 32) | w0;
+    const uint64_t hi = (uint64_t(w2) << 32) | w1;
+    const uint32_t a = uint32_t(lo >> sh);  // bytes off..off+3
+    const uint32_t b = uint32_t(hi >> sh);  // bytes off+4..off+7
+    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
+}
+
+// 16 bytes at block offset pos, zero past bl.
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* blk, uint32_t pos, uint32_t bl) {
+    if (pos + 16u <= bl) return ldg4(reinterpret_cast<const uint4*>(blk + pos));
+    uint8_t t[16];
+    for (uint32_t k = 0; k < 16; ++k) t[k] = pos + k < bl ? blk[pos + k] : 0;
+    uint4 v;
+    memcpy(&v, t, 16);
+    return v;
+}
+
+// One step of the physical-record walk (oracle walk_block rules).
+__device__ __forceinline__ uint32_t classify(const Hdr& h, uint32_t off, uint32_t bl) {
+    if (kHeaderSize + h.len > bl - off) return REVEL_REC_BAD_LENGTH;
+    if (h.type == 0 && h.len == 0) return REVEL_REC_ZERO;
+    return REVEL_REC_OK;
+}
+
+__global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t base = b * kBlockSize;
+        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
+        const uint8_t* blk = image + base;
+        uint32_t off = 0, n = 0;
+        while (bl - off >= kHeaderSize) {
+            const Hdr h = read_header(blk, off, bl);
+            ++n;
+            if (classify(h, off, bl) != REVEL_REC_OK) break;
+            off += kHeaderSize + h.len;
+        }
+        counts[b] = n;
+    }
+}
+
+// Exclusive scan, one workgroup of 1024 threads, sequential 1024-chunks.
+__global__ __launch_bounds__(1024) void k_exclusive_scan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                        uint64_t n) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry_s;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < n; base += 1024) {
+        const uint64_t i = base + threadIdx.x;
+        const uint32_t v = i < n ? in[i] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if ((int)lane_id() >= d) x += y;
+        }
+        const uint32_t w = threadIdx.x >> 6;
+        if (lane_id() == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (uint32_t k = 0; k < w; ++k) woff += wsum[k];
+        const uint32_t carry = carry_s;
+        if (i < n) out[i] = carry + woff + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry_s = carry + woff + x;
+        __syncthreads();
+    }
+}
+
+constexpr int kVerifyThreads = 512;
+constexpr uint32_t kRecCap = 256;  // records per LDS batch per wave
+
+// x^(-8 pad) mod P for pad = 0..3 (x^-1 = (P+1)/x, reflected 0x05EC76F1).
+struct InvPad {
+    uint32_t v[4];
+};
+constexpr InvPad make_inv_pad() {
+    InvPad s{};
+    const uint32_t xinv = 0x05EC76F1u;
+    uint32_t x8inv = 0x80000000u;
+    for (int k = 0; k < 8; ++k) x8inv = multmodp(x8inv, xinv);
+    uint32_t v = 0x80000000u;
+    for (int p = 0; p < 4; ++p) {
+        s.v[p] = v;
+        v = multmodp(v, x8inv);
+    }
+    return s;
+}
+static_assert(multmodp(make_inv_pad().v[1], x8n(1)) == 0x80000000u, "x^-8 * x^8 == 1");
+__constant__ InvPad c_inv_pad = make_inv_pad();
+
+struct VerifyWaveLds {
+    uint16_t s[kRecCap];    // start of the CRC range (= header offset + 6)
+    uint16_t em1[kRecCap];  // end of the range minus one (off + 7 + len - 1 <= 32767); s - 1 for bad headers
+    uint32_t acc[kRecCap];  // xor of lane contributions, aligned to E = ceil4(end)
+    uint32_t nrec;
+    uint32_t more_off;
+};
+
+// Per-lane segmented CRC.  Every record's contributions are aligned to its
+// word-aligned range end E = ceil4(e): the lane holding e absorbs the final
+// word with the bytes past e zeroed (that is R * x^(8 pad)), lanes ending
+// earlier shift their partial register by E - chunk_end; the finalizer
+// multiplies by x^(-8 pad).  Records whose header is bad get an empty range.
+__global__ __launch_bounds__(kVerifyThreads) void k_verify_records(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                                                   uint64_t base_offset,
+                                                                   const uint32_t* __restrict__ first,
+                                                                   revel_record_result* __restrict__ out) {
+    constexpr int TM = TM_S2R;
+    __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
+    fill_tables<TM>(tab);
+    __shared__ VerifyWaveLds wl_all[kVerifyThreads / 64];
+    __syncthreads();
+    VerifyWaveLds& wl = wl_all[threadIdx.x >> 6];
+    const LaneConst L = make_lane_const();
+    const uint32_t lane = lane_id();
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t waves_per_wg = kVerifyThreads / 64;
+    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+        const uint64_t base = b * kBlockSize;
+        const uint8_t* blk = image + base;
+        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
+        const uint32_t cs = lane * 512u, ce = cs + 512u;
+        uint32_t out_base = first[b];
+        uint32_t walk_from = 0;
+        for (;;) {
+            // ---- lane 0 walks up to kRecCap records into LDS ----
+            if (lane == 0) {
+                uint32_t off = walk_from, n = 0, cont = 0xFFFFFFFFu;
+                while (bl - off >= kHeaderSize) {
+                    if (n == kRecCap) { cont = off; break; }
+                    const Hdr h = read_header(blk, off, bl);
+                    const uint32_t st = classify(h, off, bl);
+                    wl.s[n] = (uint16_t)(off + 6);
+                    wl.em1[n] = (uint16_t)(st == REVEL_REC_OK ? off + kHeaderSize + h.len - 1u : off + 5u);
+                    wl.acc[n] = 0;
+                    ++n;
+                    if (st != REVEL_REC_OK) break;
+                    off += kHeaderSize + h.len;
+                }
+                wl.nrec = n;
+                wl.more_off = cont;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t nrec = wl.nrec;
+            const uint32_t cont = wl.more_off;
+
+            // Range of record k as [s, e) with exact e; E = aligned end.
+            // Bad records: s = e (empty).
+            auto load_rec = [&](uint32_t k, uint32_t& s, uint32_t& e, uint32_t& E) {
+                if (k >= nrec) { s = e = E = 0xFFFFFFFFu; return; }
+                s = wl.s[k];
+                e = uint32_t(wl.em1[k]) + 1u;
+                E = (e + 3u) & ~3u;
+            };
+            // first record whose range ends after cs (ranges are increasing)
+            uint32_t lo = 0, hi = nrec;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
+            }
+            uint32_t r = lo, s, e, E;
+            load_rec(r, s, e, E);
+            while (r < nrec && s == e) { ++r; load_rec(r, s, e, E); }
+
+            uint32_t state = 0;
+            if (cs < bl && s < ce) {
+#pragma unroll 2
+                for (uint32_t t = 0; t < 32; ++t) {
+                    const uint32_t p16 = cs + t * 16u;
+                    if (p16 >= bl || s >= ce) break;  // nothing of this batch left in the chunk
+                    const uint4 v = load16_guarded(blk, p16, bl);
+                    if (p16 >= s && p16 + 16u < e) {
+                        state = absorb4<TM>(state, v, L, tab);  // interior: no boundary in these 16 bytes
+                    } else {
+                        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t p = p16 + q * 4u;
+                            // keep bytes of [s, e) inside [p, p+4)
+                            const uint32_t lo_b = s > p ? min(s - p, 4u) : 0u;
+                            const uint32_t hi_b = e > p ? min(e - p, 4u) : 0u;
+                            uint32_t keep = hi_b >= 4u ? 0xFFFFFFFFu : ((1u << (8u * hi_b)) - 1u);
+                            keep &= lo_b >= 4u ? 0u : (0xFFFFFFFFu << (8u * lo_b));
+                            state = absorb<TM>(state, ws[q] & keep, L, tab);
+                            if (e > p && e <= p + 4u) {  // record ends in this word: flush
+                                atomicXor(&wl.acc[r], state);
+                                state = 0;
+                                do { ++r; load_rec(r, s, e, E); } while (r < nrec && s == e);
+                            }
+                        }
+                    }
+                }
+                // a record still open at the chunk end: shift to its aligned end
+                if (r < nrec && s < ce && e > ce) {
+                    atomicXor(&wl.acc[r], gf_mul(gf_x8n_block(E - ce), state));
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+
+            // ---- finalize: one lane per record ----
+            for (uint32_t k = lane; k < nrec; k += 64) {
+                const uint32_t off = uint32_t(wl.s[k]) - 6u;
+                const Hdr h = read_header(blk, off, bl);
+                const uint32_t st = classify(h, off, bl);
+                revel_record_result res;
+                res.file_offset = base_offset + base + off;
+                res.length = h.len;
+                res.stored_crc = h.stored;
+                res.type = (uint8_t)h.type;
+                res.reserved[0] = res.reserved[1] = 0;
+                if (st == REVEL_REC_OK) {
+                    const uint32_t n = h.len + 1u;  // type byte + payload
+                    const uint32_t e = off + kHeaderSize + h.len;
+                    const uint32_t pad = ((e + 3u) & ~3u) - e;
+                    const uint32_t raw = gf_mul(c_inv_pad.v[pad], wl.acc[k]);
+                    const uint32_t ix = gf_mul(gf_x8n_block(n), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+                    res.computed_crc = mask(raw ^ ix);
+                    res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
+                } else {
+                    res.computed_crc = 0;
+                    res.status = (uint8_t)st;
+                }
+                out[out_base + k] = res;
+            }
+            out_base += nrec;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (cont == 0xFFFFFFFFu) break;
+            walk_from = cont;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launch helpers
+// ---------------------------------------------------------------------------
+template <int TM, int THREADS, bool FRAME>
+hipError_t launch_full(const DeviceInfo& di, int wg_per_cu, const uint8_t* blocks, uint64_t n, uint32_t* masked,
+                       uint8_t* ok, uint8_t* frame_dst, hipStream_t st) {
+    auto kern = k_full_blocks<TM, THREADS, FRAME>;
+    const uint64_t waves_needed = n;
+    uint64_t grid = (uint64_t)di.num_cu * wg_per_cu;
+    const uint64_t wg_needed = (waves_needed + THREADS / 64 - 1) / (THREADS / 64);
+    grid = std::max<uint64_t>(1, std::min(grid, wg_needed));
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked, ok, frame_dst);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// ===========================================================================
+// Internal entry points (declared in gpu_internal.h)
+// ===========================================================================
+namespace revel {
+
+// Variant table used by the public entry point and by tools/variants.py.
+hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void* d_blocks, uint64_t n,
+                                   uint32_t* d_masked, uint8_t* d_ok, hipStream_t st) {
+    const uint8_t* b = static_cast<const uint8_t*>(d_blocks);
+    switch (variant) {
+        case 0: return launch_full<TM_S2R, 512, false>(di, 2, b, n, d_masked, d_ok, nullptr, st);
+        case 1: return launch_full<TM_S4R, 1024, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
+        case 2: return launch_full<TM_S2R, 1024, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
+        case 3: return launch_full<TM_S2R, 256, false>(di, 2, b, n, d_masked, d_ok, nullptr, st);
+        case 4: return launch_full<TM_S4, 256, false>(di, 8, b, n, d_masked, d_ok, nullptr, st);
+        case 5: return launch_full<TM_S4, 512, false>(di, 4, b, n, d_masked, d_ok, nullptr, st);
+        case 100: {
+            const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 3) / 4));
+            hipLaunchKernelGGL(k_stream_ceiling<256>, dim3((uint32_t)grid), dim3(256), 0, st, b, n, d_masked);
+            return hipGetLastError();
+        }
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st) {
+    uint8_t* b = static_cast<uint8_t*>(d_blocks);
+    return launch_full<TM_S2R, 512, true>(di, 2, b, n, nullptr, nullptr, b, st);
+}
+
+hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
+                             hipStream_t st) {
+    const uint64_t words = n * (kBlockSize / 8);
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 16, (words + 255) / 256));
+    hipLaunchKernelGGL(k_synth, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<uint64_t*>(d_blocks), n, seed,
+                       first);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return frame_full_blocks(di, d_blocks, n, st);
+}
+
+hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                         hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 4, (nblocks + 63) / 64));
+    hipLaunchKernelGGL(k_count_records, dim3((uint32_t)grid), dim3(64), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts);
+    return hipGetLastError();
+}
+
+hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_exclusive_scan, dim3(1), dim3(1024), 0, st, d_in, d_out, n);
+    return hipGetLastError();
+}
+
+hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                          const uint32_t* d_first, revel_record_result* d_out, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t waves = kVerifyThreads / 64;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 2, (nblocks + waves - 1) / waves));
+    hipLaunchKernelGGL(k_verify_records, dim3((uint32_t)grid), dim3(kVerifyThreads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out);
+    return hipGetLastError();
+}
+
+}  // namespace revel

@@ -1,0 +1,38 @@
+// gpu_internal.h -- internal interface between the C-ABI layer and the
+// gfx950 kernels in gpu_crc.hip.  Not installed; see include/revel_wal.h.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "revel_wal.h"
+
+namespace revel {
+
+struct DeviceInfo {
+    int device = 0;
+    int num_cu = 256;
+};
+
+// variant: 0 = production (S2R, 512 threads, 2 WG/CU); others are the
+// experiment arms listed in gpu_crc.hip (100 = streaming-read ceiling).
+hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void* d_blocks, uint64_t n,
+                                   uint32_t* d_masked, uint8_t* d_ok, hipStream_t st);
+hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st);
+hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
+                             hipStream_t st);
+hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                         hipStream_t st);
+hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
+                              hipStream_t st);
+hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                          const uint32_t* d_first, revel_record_result* d_out, hipStream_t st);
+
+// Set the thread-local error string; returns code.
+int set_error(int code, const char* fmt, ...);
+
+}  // namespace revel
+
+struct revel_gpu_context {
+    revel::DeviceInfo di;
+    hipStream_t stream = nullptr;
+};

@@ -1,0 +1,179 @@
+"""Device-resident CRC engine (gfx950 HIP kernels) via the C-ABI.
+
+Device memory is owned through :class:`DeviceBuffer`; host arrays are numpy.
+No torch types cross the boundary: every call hands plain pointers to
+``librevel_wal.so``.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_float, c_int, c_void_p
+from typing import Optional, Tuple
+
+import numpy as np
+
+from ._lib import BLOCK_SIZE, RecordResult, check, lib
+
+RECORD_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("stored_crc", "<u4"),
+                         ("computed_crc", "<u4"), ("type", "u1"), ("status", "u1"), ("reserved", "u1", (2,))])
+assert RECORD_DTYPE.itemsize == ctypes.sizeof(RecordResult)
+
+
+def device_count() -> int:
+    n = c_int(0)
+    check(lib().revel_gpu_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: "GpuContext", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = nbytes
+        p = c_void_p()
+        check(lib().revel_gpu_malloc(ctx.handle, nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def free(self) -> None:
+        if self.ptr:
+            check(lib().revel_gpu_free(self.ctx.handle, self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def offset(self, nbytes: int) -> int:
+        return self.ptr + nbytes
+
+
+class Event:
+    def __init__(self, ctx: "GpuContext"):
+        self.ctx = ctx
+        p = c_void_p()
+        check(lib().revel_gpu_event_new(ctx.handle, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def record(self, stream: Optional[int] = None) -> None:
+        check(lib().revel_gpu_event_record(self.ctx.handle, self.ptr, stream))
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = c_float()
+        check(lib().revel_gpu_event_elapsed_ms(self.ctx.handle, self.ptr, end.ptr, ctypes.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().revel_gpu_event_free(self.ctx.handle, self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+class GpuContext:
+    """One HIP device + stream (``revel_gpu_context``)."""
+
+    def __init__(self, device: int = 0):
+        p = c_void_p()
+        check(lib().revel_gpu_context_new(device, ctypes.byref(p)))
+        self._h = p.value
+        self.device = device
+
+    @property
+    def handle(self) -> int:
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return lib().revel_gpu_context_stream(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            lib().revel_gpu_context_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- plumbing ----
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def h2d(self, dst: DeviceBuffer, src: np.ndarray, dst_offset: int = 0) -> None:
+        src = np.ascontiguousarray(src)
+        check(lib().revel_gpu_memcpy_h2d(self._h, dst.ptr + dst_offset, src.ctypes.data, src.nbytes, None))
+        self.sync()
+
+    def d2h(self, src: DeviceBuffer, nbytes: int, dtype=np.uint8, src_offset: int = 0) -> np.ndarray:
+        out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype=dtype)
+        check(lib().revel_gpu_memcpy_d2h(self._h, out.ctypes.data, src.ptr + src_offset, out.nbytes, None))
+        self.sync()
+        return out
+
+    def upload(self, host: np.ndarray) -> DeviceBuffer:
+        host = np.ascontiguousarray(host)
+        buf = self.alloc(max(1, host.nbytes))
+        if host.nbytes:
+            self.h2d(buf, host)
+        return buf
+
+    def memset(self, dst: DeviceBuffer, value: int, nbytes: int) -> None:
+        check(lib().revel_gpu_memset(self._h, dst.ptr, value, nbytes, None))
+
+    def sync(self) -> None:
+        check(lib().revel_gpu_stream_synchronize(self._h, None))
+
+    def event(self) -> Event:
+        return Event(self)
+
+    # ---- kernels ----
+    def crc_full_blocks(self, blocks: DeviceBuffer, nblocks: int, masked_out: DeviceBuffer,
+                        ok_out: Optional[DeviceBuffer] = None, variant: Optional[int] = None) -> None:
+        """Config C2: masked CRC of bytes [6:32768) of each full-type block."""
+        if blocks.nbytes < nblocks * BLOCK_SIZE or masked_out.nbytes < 4 * nblocks:
+            raise ValueError("buffer too small for nblocks")
+        if ok_out is not None and ok_out.nbytes < nblocks:
+            raise ValueError("ok buffer too small")
+        ok = ok_out.ptr if ok_out is not None else None
+        if variant is None:
+            check(lib().revel_gpu_crc_full_blocks(self._h, blocks.ptr, nblocks, masked_out.ptr, ok, None))
+        else:
+            check(lib().revel_gpu_crc_full_blocks_variant(self._h, variant, blocks.ptr, nblocks,
+                                                          masked_out.ptr, ok, None))
+
+    def frame_full_blocks(self, blocks: DeviceBuffer, nblocks: int) -> None:
+        if blocks.nbytes < nblocks * BLOCK_SIZE:
+            raise ValueError("buffer too small for nblocks")
+        check(lib().revel_gpu_frame_full_blocks(self._h, blocks.ptr, nblocks, None))
+
+    def synth_full_blocks(self, blocks: DeviceBuffer, nblocks: int, seed: int, first: int = 0) -> None:
+        if blocks.nbytes < nblocks * BLOCK_SIZE:
+            raise ValueError("buffer too small for nblocks")
+        check(lib().revel_gpu_synth_full_blocks(self._h, blocks.ptr, nblocks, seed, first, None))
+
+    def verify_image(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0) -> np.ndarray:
+        """Config C3: walk + CRC every physical record of a device-resident
+        WAL image.  Returns a structured array (RECORD_DTYPE) in file order."""
+        if nbytes == 0:
+            return np.zeros(0, dtype=RECORD_DTYPE)
+        if image.nbytes < nbytes:
+            raise ValueError("image buffer smaller than nbytes")
+        nblocks = (nbytes + BLOCK_SIZE - 1) // BLOCK_SIZE
+        counts = self.alloc(4 * nblocks)
+        first = self.alloc(4 * nblocks)
+        L = lib()
+        check(L.revel_gpu_count_records(self._h, image.ptr, nbytes, counts.ptr, None))
+        check(L.revel_gpu_exclusive_scan_u32(self._h, counts.ptr, first.ptr, nblocks, None))
+        tail_first = self.d2h(first, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
+        tail_count = self.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
+        total = int(tail_first) + int(tail_count)
+        out = self.alloc(max(1, total) * RECORD_DTYPE.itemsize)
+        check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
+        self.sync()
+        res = self.d2h(out, total * RECORD_DTYPE.itemsize, np.uint8).view(RECORD_DTYPE)
+        return res

@@ -1,0 +1,172 @@
+"""The C-ABI library on the CPU: symbol surface, host CRC, writer, files and
+the checksum=False reader, all against the oracle and the golden fixtures.
+No compute is sent to a GPU here."""
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import revel_amd
+from revel_amd import _lib, crc, env, gpu, log
+from revel_amd._lib import RevelError
+from conftest import ROOT, golden_image
+from oracle import crc32c_oracle as po
+from oracle import oracle_c as oc
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "revel_wal.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(revel_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    L = revel_amd.lib()
+    syms = header_symbols()
+    assert len(syms) >= 45
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+
+
+def test_gpu_entry_points_fail_loudly_without_device():
+    if gpu.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RevelError) as e:
+        gpu.GpuContext(0)
+    assert e.value.code == _lib.NOT_SUPPORT
+    # checksum verification needs the GPU: no silent CPU fallback
+    f = env.MemorySequentialFile(b"")
+    with pytest.raises(RevelError) as e:
+        log.Reader(f, checksum=True)
+    assert e.value.code == _lib.NOT_SUPPORT
+
+
+def test_host_crc_matches_oracle_and_kats():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "kat.json")) as f:
+        kat = json.load(f)
+    for v in kat["value"]:
+        assert crc.value(bytes.fromhex(v["data_hex"])) == v["crc"]
+    assert crc.value(b"hello world") == crc.extend(ord("h"), b"ello world")
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 5, 8, 9, 63, 64, 65, 777, 32761, 100000]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert crc.value(d) == oc.value(d)
+        assert crc.extend(n & 0xFF, d) == oc.extend(n & 0xFF, d)
+        c = crc.value(d)
+        assert crc.mask(c) == po.mask(c) and crc.unmask(crc.mask(c)) == c
+
+
+def write_mem(records, block_offset=0):
+    f = env.MemoryWritableFile()
+    w = log.Writer(f, block_offset)
+    for r in records:
+        w.add_record(r)
+    return f.contents()
+
+
+def test_writer_hello_world_golden():
+    assert write_mem([b"hello world"]) == golden_image("hello_world")
+
+
+def test_writer_matches_every_golden_edge(golden_index):
+    from tests_gen import edge_records
+    for name, ent in golden_index.items():
+        recs = edge_records(name)
+        img = write_mem(recs, ent["block_offset"])
+        if ent["post"] is None:
+            assert hashlib.sha256(img).hexdigest() == ent["sha256"], name
+        else:
+            assert img == po.write_image(recs, ent["block_offset"]), name
+
+
+def test_writer_random_vs_oracle():
+    rng = np.random.default_rng(4)
+    for trial in range(5):
+        sizes = rng.integers(0, 80000, 30)
+        recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+        boff = int(rng.integers(0, 32768))
+        assert write_mem(recs, boff) == oc.write_image(recs, boff)
+
+
+def test_writer_c1_golden_digest():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c1_records.npz"))
+    words = po.splitmix64_np(np.uint64(0x5EED0001) ^ np.arange(10000, dtype=np.uint64), 512)
+    img = write_mem([words[i].tobytes() for i in range(10000)])
+    assert len(img) == 41038750
+    assert hashlib.sha256(img).digest() == z["sha256"].tobytes()
+
+
+def test_posix_files_roundtrip(tmp_path):
+    path = str(tmp_path / "000001.log")
+    f = env.PosixWritableFile(path)
+    w = log.Writer(f)
+    recs = [b"a" * 10, b"b" * 70000, b"", b"c" * 200000]
+    for r in recs:
+        w.add_record(r)
+    f.sync()
+    f.close()
+    with open(path, "rb") as fh:
+        data = fh.read()
+    assert data == oc.write_image(recs)  # (the reference's Posix file writes zeros: App. A #4)
+    s = env.PosixSequentialFile(path)
+    assert s.read(7) == data[:7]
+    s.skip(10)
+    assert s.read(5) == data[17:22]
+    rd = log.Reader(env.PosixSequentialFile(path), checksum=False)
+    assert list(rd) == recs
+
+
+def test_posix_missing_file_is_not_found(tmp_path):
+    with pytest.raises(RevelError) as e:
+        env.PosixSequentialFile(str(tmp_path / "nope.log"))
+    assert e.value.code == _lib.NOT_FOUND
+
+
+def test_memory_sequential_file_semantics():
+    s = env.MemorySequentialFile(b"0123456789")
+    assert s.read(3) == b"012"
+    s.skip(2)  # relative
+    assert s.read(100) == b"56789"
+    assert s.read(4) == b""
+
+
+def test_reader_nochecksum_all_golden(golden_index):
+    for name, ent in golden_index.items():
+        img = golden_image(name)
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=False, window_bytes=65536)
+        try:
+            got = list(rd)
+        except RevelError:
+            got = "error"
+        try:
+            want = po.read_all(img, checksum=False)
+        except po.CorruptionError:
+            want = "error"
+        if want == "error":
+            assert got == "error", name
+        else:
+            assert got == want, name
+
+
+@pytest.mark.parametrize("window", [32768, 65536, 1 << 20])
+def test_reader_windows_and_fragments(window):
+    rng = np.random.default_rng(5)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 150000, 40)]
+    img = oc.write_image(recs)
+    rd = log.Reader(env.MemorySequentialFile(img), checksum=False, window_bytes=window)
+    assert list(rd) == recs
+
+
+def test_reader_initial_offset():
+    recs = [bytes([i]) * 20000 for i in range(10)]
+    img = oc.write_image(recs)
+    for off in [0, 1, 20007, 32768, 40000, 100000, len(img)]:
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=False, initial_offset=off)
+        got = list(rd)
+        want = po.read_all(img, checksum=False, initial_offset=off)
+        assert got == want, off
