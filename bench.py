@@ -1,0 +1,227 @@
+"""Benchmark: CRC32C GiB/s on device-resident 32 KiB WAL blocks (config C2).
+
+One step = one launch of the production CRC kernel over every block resident
+in HBM (compute the masked CRC32C of type||payload of each full-type block and
+verify it against the stored header).  Per rank: 1 M blocks = 32 GiB,
+synthesised and framed on the device (splitmix64 payloads).  Ranks are
+independent WAL streams, one per GPU, no collective on the data path
+("scaling": "weak"); the barrier / max-over-ranks uses gloo on the host.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints one JSON line on rank 0.  The `cpu_baseline` leg (rank 0, N=1) times
+the oracle's bytewise table CRC -- the reference crate's algorithm class --
+on a bounded sample of the same blocks, on one host core, and checks the
+GPU's CRCs for that sample against it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# The product library (and its HIP runtime) is loaded before anything else.
+from revel_amd import BLOCK_SIZE, gpu  # noqa: E402
+
+METRIC = "CRC32C GiB/s on device-resident 32 KiB WAL blocks; % of HBM-read roofline"
+PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SEED = 0x5EED0002
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per rank (default 1M = 32 GiB)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound on the CPU baseline leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", 0))
+        self.world = int(os.environ.get("WORLD_SIZE", 1))
+        self.local = int(os.environ.get("LOCAL_RANK", 0))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist  # host-side gloo only; torch never touches the GPU here
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def pmc_traffic(nblocks: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass, if one was
+    taken for this workload (profiles/pmc_c2.json, written by
+    tools/pmc_summary.py), else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_c2.json")
+    try:
+        with open(path) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if int(p.get("blocks", -1)) != nblocks:
+        return None
+    return p.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
+    """Oracle bytewise CRC (reference algorithm class) on one host core, over a
+    bounded sample of the same device blocks; also the parity check of the
+    GPU CRCs on that sample."""
+    from oracle import oracle_c  # checker / baseline only
+
+    stride = max(1, nblocks // 4096)
+    idx = np.arange(0, nblocks, stride)[:4096]
+    sample = np.stack([ctx.d2h(dblocks, BLOCK_SIZE, src_offset=int(i) * BLOCK_SIZE) for i in idx])
+    gpu_crc = ctx.d2h(masked_dev, 4 * nblocks, np.uint32)[idx]
+    # bytewise (reference-equivalent) timed leg, bounded by `seconds`
+    done, t0 = 0, time.perf_counter()
+    want = np.empty(len(idx), np.uint32)
+    while done < len(idx) and time.perf_counter() - t0 < seconds:
+        k = min(64, len(idx) - done)
+        want[done:done + k] = oracle_c.full_block_crcs(sample[done:done + k], "bytewise")
+        done += k
+    t_byte = time.perf_counter() - t0
+    parity = bool(np.array_equal(want[:done], gpu_crc[:done]))
+    ctxt = {}
+    for v in ("slice16", "sse42"):
+        t0 = time.perf_counter()
+        got = oracle_c.full_block_crcs(sample, v)
+        ctxt[v] = round(len(idx) * BLOCK_SIZE / 2**30 / (time.perf_counter() - t0), 3)
+        parity = parity and bool(np.array_equal(got, gpu_crc))
+    return {
+        "value": round(done * BLOCK_SIZE / 2**30 / t_byte, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done} of the {nblocks} benchmark blocks (every {stride}th), oracle bytewise 256-entry "
+                  f"table CRC (crate `crc` algorithm class), single thread, {t_byte:.1f} s",
+        "context_GiB_s_1core": ctxt,
+        "host_cores_available": os.cpu_count(),
+        "parity_vs_gpu": parity,
+    }
+
+
+def main():
+    args = parse()
+    D = Dist()
+    ctx = gpu.GpuContext(D.local)
+    n = args.blocks
+    dblocks = ctx.alloc(n * BLOCK_SIZE)
+    masked = ctx.alloc(4 * n)
+    ok = ctx.alloc(n)
+    ctx.synth_full_blocks(dblocks, n, seed=SEED ^ (D.rank << 40))
+    ctx.sync()
+
+    def step():
+        ctx.crc_full_blocks(dblocks, n, masked, ok, variant=args.variant)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    okh = ctx.d2h(ok, n)
+    all_ok = D.sum(float(okh.all())) == D.world
+
+    ev0, ev1 = ctx.event(), ctx.event()
+    ctx.sync()
+    D.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    ctx.sync()
+    D.barrier()
+    t1 = time.perf_counter()
+    wall = D.max(t1 - t0)
+    kern_ms = ev0.elapsed_ms(ev1) / args.steps
+    kern_ms_max = D.max(kern_ms)
+
+    total_blocks = n * D.world
+    value = total_blocks * BLOCK_SIZE / 2**30 / (wall / args.steps)
+    alg_bytes = n * (BLOCK_SIZE + 4 + 1)          # read block, write masked CRC + ok flag
+    achieved = alg_bytes / (kern_ms_max / 1e3) / 1e9
+    traffic = pmc_traffic(n)
+
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(ctx, dblocks, masked, n, args.cpu_seconds)
+
+    if D.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "GiB/s",
+            "n_gpus": D.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: splitmix64 payloads generated + framed (masked CRC headers) on device",
+            "config": {
+                "workload": "C2: device-resident full-type 32 KiB WAL blocks, masked CRC32C(type||payload) "
+                            "compute + verify vs stored header, one wavefront per block",
+                "blocks_per_gpu": n,
+                "bytes_per_gpu": n * BLOCK_SIZE,
+                "parallelism": f"independent WAL stream per GPU x{D.world} (no collective)",
+                "kernel_variant": "production" if args.variant is None else args.variant,
+                "all_verify_flags_ok": all_ok,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kern_ms_max, 4),
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

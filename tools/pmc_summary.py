@@ -1,0 +1,73 @@
+"""Summarise rocprofv3 PMC csv passes: per kernel, mean of each counter.
+
+usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [--json out.json --blocks N --kernel SUBSTR]
+FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half of
+a wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), so
+hbm_read_bytes = 2 * FETCH_SIZE * 1024 for those kernels.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    m = re.search(r"(k_\w+)(<[^>]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
+def load(d):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv"))):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                acc[k]["_dur_ns"].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--json")
+    ap.add_argument("--blocks", type=int, default=1 << 20)
+    ap.add_argument("--kernel", default="k_full_blocks<0, 1024, 1, false>")
+    a = ap.parse_args()
+    res = load(a.dir)
+    for k, cs in res.items():
+        print(f"== {k}")
+        for c, v in sorted(cs.items()):
+            print(f"   {c:32s} {v:16.1f}")
+        if "SQ_WAVE_CYCLES" in cs and cs["SQ_WAVE_CYCLES"]:
+            w = cs["SQ_WAVE_CYCLES"]
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                      "SQ_ACTIVE_INST_LDS"):
+                if c in cs:
+                    print(f"   share {c:26s} {cs[c] / w:8.3f}")
+        if "GRBM_GUI_ACTIVE" in cs:
+            print(f"   eff clock GHz ~ {cs['GRBM_GUI_ACTIVE'] / 8 / cs['_dur_ns']:.3f}")
+    if a.json:
+        cs = res.get(a.kernel)
+        if cs is None:
+            raise SystemExit(f"kernel {a.kernel} not found; have {list(res)}")
+        fetch = cs.get("FETCH_SIZE")
+        write = cs.get("WRITE_SIZE")
+        out = {"kernel": a.kernel, "blocks": a.blocks,
+               "fetch_size_kib": fetch, "write_size_kib": write,
+               "hbm_read_bytes_per_launch": None if fetch is None else 2 * fetch * 1024,
+               "hbm_write_bytes_per_launch": None if write is None else write * 1024,
+               "correction": "gfx950: FETCH_SIZE x2 for wide coalesced reads (MI355X_MICROARCH.md HBM); "
+                             "WRITE_SIZE x1",
+               "counters": cs}
+        if fetch is not None and write is not None:
+            out["hbm_bytes_per_launch"] = out["hbm_read_bytes_per_launch"] + out["hbm_write_bytes_per_launch"]
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

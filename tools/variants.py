@@ -20,7 +20,7 @@ from revel_amd import BLOCK_SIZE, gpu  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=1 << 20)
-    ap.add_argument("--variants", default="100,0,1,2,3,4,5")
+    ap.add_argument("--variants", default="100,0,1,2,3,4,5,6,7")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     args = ap.parse_args()
