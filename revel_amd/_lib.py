@@ -87,6 +87,8 @@ SIGNATURES = {
 
 # exported experiment hooks (not part of the public header)
 EXTRA_SIGNATURES = {
+    "revel_gpu_verify_records_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
+                                                 c_void_p, c_void_p]),
     "revel_gpu_crc_full_blocks_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p,
                                                   c_void_p]),
 }

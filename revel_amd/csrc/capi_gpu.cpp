@@ -187,6 +187,19 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     return REVEL_OK;
 }
 
+// Experiment hook (not in the public header): 0 = production, 1 = round-1 kernel.
+int revel_gpu_verify_records_variant(revel_gpu_context* ctx, int variant, const void* d_image, size_t nbytes,
+                                     uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                     void* stream) {
+    CHECK_CTX(ctx);
+    if (nbytes == 0) return REVEL_OK;
+    if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    HIP_TRY(revel::verify_records_variant(ctx->di, variant, d_image, nbytes, base_offset, d_first, d_out,
+                                          pick(ctx, stream)),
+            "verify_records_variant launch");
+    return REVEL_OK;
+}
+
 int revel_gpu_malloc(revel_gpu_context* ctx, size_t n, void** d_ptr) {
     CHECK_CTX(ctx);
     if (!d_ptr) return set_error(REVEL_INVALID_ARGUMENT, "null out");

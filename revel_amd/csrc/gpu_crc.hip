@@ -634,6 +634,189 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify_records(const uint8_t
 }
 
 // ---------------------------------------------------------------------------
+// Config C3, v2: S4R tables, 16 waves/CU, pipelined loads, wave-uniform fast
+// path, exact tails.
+// ---------------------------------------------------------------------------
+constexpr int kVerify2Threads = 1024;
+constexpr uint32_t kRecCap2 = 128;
+
+// x^(8d) and init_xor(d) for d = 0..32768, filled once per device.
+__device__ uint32_t g_x8n_tab[kBlockSize + 1];
+__device__ uint32_t g_init_xor_tab[kBlockSize + 1];
+
+__global__ void k_init_len_tables() {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d <= kBlockSize; d += gridDim.x * blockDim.x) {
+        const uint32_t x = gf_x8n_block(d);
+        g_x8n_tab[d] = x;
+        g_init_xor_tab[d] = gf_mul(x, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    }
+}
+
+struct VerifyWaveLds2 {
+    uint16_t s[kRecCap2];
+    uint16_t em1[kRecCap2];  // end - 1; s - 1 for a bad header (empty range)
+    uint32_t acc[kRecCap2];
+    uint32_t nrec, more_off;
+};
+
+// One CRC step over a single byte with the S4R image's T0 (region 1, half 1).
+__device__ __forceinline__ uint32_t byte_step_s4r(uint32_t state, uint32_t b, LaneConst L, const uint32_t* tab) {
+    const uint32_t x = state ^ b;
+    const uint32_t a = __builtin_amdgcn_perm(x, L.lc1, Sel<0>::v);
+    return ldsw<128>(tab, a) ^ (state >> 8);
+}
+
+__global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                                                     uint64_t base_offset,
+                                                                     const uint32_t* __restrict__ first,
+                                                                     revel_record_result* __restrict__ out) {
+    __shared__ uint32_t tab[32768];
+    __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
+    fill_tables<TM_S4R>(tab);
+    __syncthreads();
+    VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
+    const LaneConst L = make_lane_const();
+    const uint32_t lane = lane_id();
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t waves_per_wg = kVerify2Threads / 64;
+    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+        const uint64_t base = b * kBlockSize;
+        const uint8_t* blk = image + base;
+        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
+        const bool full = bl == kBlockSize;
+        const uint32_t cs = lane * 512u, ce = cs + 512u;
+        uint32_t out_base = first[b];
+        uint32_t walk_from = 0;
+        for (;;) {
+            if (lane == 0) {
+                uint32_t off = walk_from, n = 0, cont = kNone;
+                while (bl - off >= kHeaderSize) {
+                    if (n == kRecCap2) { cont = off; break; }
+                    const Hdr h = read_header(blk, off, bl);
+                    const uint32_t st = classify(h, off, bl);
+                    wl.s[n] = (uint16_t)(off + 6);
+                    wl.em1[n] = (uint16_t)(st == REVEL_REC_OK ? off + kHeaderSize + h.len - 1u : off + 5u);
+                    wl.acc[n] = 0;
+                    ++n;
+                    if (st != REVEL_REC_OK) break;
+                    off += kHeaderSize + h.len;
+                }
+                wl.nrec = n;
+                wl.more_off = cont;
+            }
+            wave_lds_sync();
+            const uint32_t nrec = wl.nrec;
+            const uint32_t cont = wl.more_off;
+            auto load_rec = [&](uint32_t k, uint32_t& s, uint32_t& e) {
+                if (k >= nrec) { s = e = kNone; return; }
+                s = wl.s[k];
+                e = uint32_t(wl.em1[k]) + 1u;
+            };
+            uint32_t lo = 0, hi = nrec;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
+            }
+            uint32_t r = lo, s, e;
+            load_rec(r, s, e);
+            while (r < nrec && s == e) { ++r; load_rec(r, s, e); }
+            const uint32_t rec_lo = __builtin_amdgcn_readfirstlane(lo);
+            const bool active = cs < bl && r < nrec && s < ce;
+            uint32_t state = 0;
+            if (__any(active)) {
+                auto load_round = [&](uint4* v, int rr) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t pos = cs + rr * 128 + j * 16;
+                        v[j] = full ? ldg4_plain(reinterpret_cast<const uint4*>(blk + pos))
+                                    : (pos < bl ? load16_guarded(blk, pos, bl) : make_uint4(0, 0, 0, 0));
+                    }
+                };
+                uint4 cur[8], nxt[8];
+                load_round(cur, 0);
+#pragma unroll 1
+                for (int rr = 0; rr < 4; ++rr) {
+                    if (rr < 3) load_round(nxt, rr + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t p16 = cs + rr * 128 + j * 16;
+                        // don't-care gap before the next record, or strictly inside one
+                        const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
+                        if (__all(interior)) {
+                            state = absorb4<TM_S4R>(state, cur[j], L, tab);
+                        } else {
+                            const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const uint32_t p = p16 + q * 4u;
+                                const uint32_t w = ws[q];
+                                if (s >= p + 4u) {
+                                    // gap word (or no record left): state is don't-care
+                                } else if (e > p + 4u) {
+                                    // record continues past this word; maybe starts in it
+                                    if (s >= p) state = 0;
+                                    const uint32_t lb = s > p ? s - p : 0u;
+                                    state = absorb<TM_S4R>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
+                                } else if (e > p) {
+                                    // record ends in this word (and may start in it)
+                                    if (s >= p) state = 0;
+                                    const uint32_t lb = s > p ? s - p : 0u;
+                                    const uint32_t hb = e - p;
+                                    if (lb == 0 && hb == 4) {
+                                        state = absorb<TM_S4R>(state, w, L, tab);
+                                    } else {
+                                        for (uint32_t t = lb; t < hb; ++t)
+                                            state = byte_step_s4r(state, (w >> (8u * t)) & 0xffu, L, tab);
+                                    }
+                                    atomicXor(&wl.acc[r], state);
+                                    state = 0;
+                                    do { ++r; load_rec(r, s, e); } while (r < nrec && s == e);
+                                }
+                            }
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+                }
+                // record still open at the chunk end: shift its partial register to e
+                if (cs < bl && r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[e - ce], state));
+            }
+            (void)rec_lo;
+            wave_lds_sync();
+            for (uint32_t k = lane; k < nrec; k += 64) {
+                const uint32_t off = uint32_t(wl.s[k]) - 6u;
+                const Hdr h = read_header(blk, off, bl);
+                const uint32_t st = classify(h, off, bl);
+                revel_record_result res;
+                res.file_offset = base_offset + base + off;
+                res.length = h.len;
+                res.stored_crc = h.stored;
+                res.type = (uint8_t)h.type;
+                res.reserved[0] = res.reserved[1] = 0;
+                if (st == REVEL_REC_OK) {
+                    res.computed_crc = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                    res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
+                } else {
+                    res.computed_crc = 0;
+                    res.status = (uint8_t)st;
+                }
+                out[out_base + k] = res;
+            }
+            out_base += nrec;
+            wave_lds_sync();
+            if (cont == kNone) break;
+            walk_from = cont;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Launch helpers
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
@@ -1046,14 +1229,35 @@ hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t*
     return hipGetLastError();
 }
 
-hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                          const uint32_t* d_first, revel_record_result* d_out, hipStream_t st) {
+hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
+                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                  hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    const uint64_t waves = kVerifyThreads / 64;
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 2, (nblocks + waves - 1) / waves));
-    hipLaunchKernelGGL(k_verify_records, dim3((uint32_t)grid), dim3(kVerifyThreads), 0, st,
+    if (variant == 1) {
+        const uint64_t waves = kVerifyThreads / 64;
+        const uint64_t grid =
+            std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 2, (nblocks + waves - 1) / waves));
+        hipLaunchKernelGGL(k_verify_records, dim3((uint32_t)grid), dim3(kVerifyThreads), 0, st,
+                           static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out);
+        return hipGetLastError();
+    }
+    static thread_local int inited_dev = -1;
+    if (inited_dev != di.device) {  // one-time per device (per thread): x^(8d), init_xor(d) tables
+        hipLaunchKernelGGL(k_init_len_tables, dim3(64), dim3(256), 0, st);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        inited_dev = di.device;
+    }
+    const uint64_t waves = kVerify2Threads / 64;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
+    hipLaunchKernelGGL(k_verify_records2, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
                        static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out);
     return hipGetLastError();
+}
+
+hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                          const uint32_t* d_first, revel_record_result* d_out, hipStream_t st) {
+    return verify_records_variant(di, 0, d_image, nbytes, base_offset, d_first, d_out, st);
 }
 
 }  // namespace revel

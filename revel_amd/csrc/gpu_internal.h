@@ -24,6 +24,9 @@ hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nby
                          hipStream_t st);
 hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
                               hipStream_t st);
+hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
+                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                  hipStream_t st);
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, hipStream_t st);
 

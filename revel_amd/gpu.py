@@ -156,7 +156,8 @@ class GpuContext:
             raise ValueError("buffer too small for nblocks")
         check(lib().revel_gpu_synth_full_blocks(self._h, blocks.ptr, nblocks, seed, first, None))
 
-    def verify_image(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0) -> np.ndarray:
+    def verify_image(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0,
+                     variant: Optional[int] = None) -> np.ndarray:
         """Config C3: walk + CRC every physical record of a device-resident
         WAL image.  Returns a structured array (RECORD_DTYPE) in file order."""
         if nbytes == 0:
@@ -173,7 +174,11 @@ class GpuContext:
         tail_count = self.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         total = int(tail_first) + int(tail_count)
         out = self.alloc(max(1, total) * RECORD_DTYPE.itemsize)
-        check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
+        if variant is None:
+            check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
+        else:
+            check(L.revel_gpu_verify_records_variant(self._h, variant, image.ptr, nbytes, base_offset, first.ptr,
+                                                     out.ptr, None))
         self.sync()
         res = self.d2h(out, total * RECORD_DTYPE.itemsize, np.uint8).view(RECORD_DTYPE)
         return res

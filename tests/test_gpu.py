@@ -124,11 +124,15 @@ def compare_walk(res, ref):
         assert np.array_equal(res[f].astype(np.uint64), ref[f].astype(np.uint64)), f
 
 
-def test_verify_golden_images(gpu_ctx, golden_index):
+VERIFY_VARIANTS = [0, 1]
+
+
+@pytest.mark.parametrize("variant", VERIFY_VARIANTS)
+def test_verify_golden_images(gpu_ctx, golden_index, variant):
     for name in golden_index:
         img = golden_image(name)
         dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-        res = gpu_ctx.verify_image(dimg, len(img))
+        res = gpu_ctx.verify_image(dimg, len(img), variant=variant)
         compare_walk(res, oc.walk(img))
 
 
@@ -145,7 +149,8 @@ def zipf_image(rng, nbytes_target):
     return recs
 
 
-def test_verify_zipf_and_corruption(gpu_ctx):
+@pytest.mark.parametrize("variant", VERIFY_VARIANTS)
+def test_verify_zipf_and_corruption(gpu_ctx, variant):
     rng = np.random.default_rng(13)
     recs = zipf_image(rng, 16 << 20)
     img = bytearray(oc.write_image(recs))
@@ -158,20 +163,32 @@ def test_verify_zipf_and_corruption(gpu_ctx):
         img[off] ^= 1 << int(rng.integers(0, 8))
     img = bytes(img)
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    res = gpu_ctx.verify_image(dimg, len(img), base_offset=0)
+    res = gpu_ctx.verify_image(dimg, len(img), base_offset=0, variant=variant)
     ref2 = oc.walk(img)
     compare_walk(res, ref2)
     assert sorted(np.flatnonzero(res["status"] == 1).tolist()) == sorted(victims.tolist())
 
 
+@pytest.mark.parametrize("variant", VERIFY_VARIANTS)
 @pytest.mark.parametrize("cut", [1, 3, 6, 7, 8, 100, 32767, 32769, 40000])
-def test_verify_partial_last_block(gpu_ctx, cut):
+def test_verify_partial_last_block(gpu_ctx, cut, variant):
     rng = np.random.default_rng(cut)
     recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 9000, 30)]
     img = oc.write_image(recs)
     img = img[:min(len(img), cut + 65536)]
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    compare_walk(gpu_ctx.verify_image(dimg, len(img)), oc.walk(img))
+    compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=variant), oc.walk(img))
+
+
+def test_verify_small_records_dense(gpu_ctx):
+    """Thousands of tiny records per block (many batches of the LDS record
+    list, record starts/ends in every lane) in random bit positions."""
+    rng = np.random.default_rng(15)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 40, 20000)]
+    img = oc.write_image(recs)
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    for v in VERIFY_VARIANTS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), oc.walk(img))
 
 
 def test_verify_base_offset_and_random_bytes(gpu_ctx):

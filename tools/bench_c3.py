@@ -50,6 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--variants", default="0,1")
     a = ap.parse_args()
     t0 = time.time()
     img = make_image(a.bytes)
@@ -66,26 +67,30 @@ def main():
     out = ctx.alloc(nrec * 24)
     L = lib()
     e0, e1, e2 = ctx.event(), ctx.event(), ctx.event()
-    times_all, times_verify = [], []
-    for _ in range(a.iters):
-        e0.record()
-        check(L.revel_gpu_count_records(ctx.handle, d.ptr, n, counts.ptr, None))
-        check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
-        e1.record()
-        check(L.revel_gpu_verify_records(ctx.handle, d.ptr, n, 0, first.ptr, out.ptr, None))
-        e2.record()
-        ctx.sync()
-        times_all.append(e0.elapsed_ms(e2))
-        times_verify.append(e1.elapsed_ms(e2))
-    ta, tv = float(np.median(times_all)), float(np.median(times_verify))
-    print(json.dumps({
-        "workload": "C3 zipf 64B-32KiB records, device walk + segmented CRC verify",
-        "image_bytes": n, "blocks": nblocks, "physical_records": nrec, "bad_records": bad,
-        "types": {int(t): int((res["type"] == t).sum()) for t in (1, 2, 3, 4)},
-        "host_write_s": round(t_write, 2),
-        "ms_count_scan_verify": round(ta, 4), "ms_verify_only": round(tv, 4),
-        "GiB_s_total": round(n / 2**30 / (ta / 1e3), 1), "GiB_s_verify": round(n / 2**30 / (tv / 1e3), 1),
-    }), flush=True)
+    for variant in [int(v) for v in a.variants.split(",")]:
+        times_all, times_verify = [], []
+        for _ in range(a.iters):
+            e0.record()
+            check(L.revel_gpu_count_records(ctx.handle, d.ptr, n, counts.ptr, None))
+            check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+            e1.record()
+            check(L.revel_gpu_verify_records_variant(ctx.handle, variant, d.ptr, n, 0, first.ptr, out.ptr, None))
+            e2.record()
+            ctx.sync()
+            times_all.append(e0.elapsed_ms(e2))
+            times_verify.append(e1.elapsed_ms(e2))
+        got = ctx.d2h(out, nrec * 24, np.uint8).view(res.dtype)
+        same = bool(np.array_equal(got, res))
+        ta, tv = float(np.median(times_all)), float(np.median(times_verify))
+        print(json.dumps({
+            "workload": "C3 zipf 64B-32KiB records, device walk + segmented CRC verify",
+            "verify_variant": variant, "matches_production": same,
+            "image_bytes": n, "blocks": nblocks, "physical_records": nrec, "bad_records": bad,
+            "types": {int(t): int((res["type"] == t).sum()) for t in (1, 2, 3, 4)},
+            "host_write_s": round(t_write, 2),
+            "ms_count_scan_verify": round(ta, 4), "ms_verify_only": round(tv, 4),
+            "GiB_s_total": round(n / 2**30 / (ta / 1e3), 1), "GiB_s_verify": round(n / 2**30 / (tv / 1e3), 1),
+        }), flush=True)
 
 
 if __name__ == "__main__":
