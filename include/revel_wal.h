@@ -201,6 +201,35 @@ int revel_gpu_event_free(revel_gpu_context* ctx, void* ev);
 /* Human-readable description of the last error on this thread. */
 const char* revel_last_error(void);
 
+/* ---- end-to-end replay: host bytes -> pinned ring -> HBM -> verify ------ */
+/* Replays a WAL held in a host file (or host memory) through the GPU: a ring
+ * of `nbuffers` pinned windows is filled by `io_threads` host threads (pread /
+ * memcpy), each window is copied to HBM on a copy stream and verified on the
+ * context's stream while the next windows are read and copied; only a small
+ * per-window summary returns to the host.  This is the end-to-end rate of
+ * log_reader.rs's path (env.rs:162-169 read(2) -> CRC), PCIe-inclusive.
+ * mode REVEL_REPLAY_RECORDS verifies every physical record (config C3/C5
+ * layout); REVEL_REPLAY_FULL_BLOCKS treats every block as one FULL record
+ * (config C2 layout).  Windows are whole blocks; records never cross a block,
+ * so window boundaries are exact. */
+#define REVEL_REPLAY_RECORDS 0
+#define REVEL_REPLAY_FULL_BLOCKS 1
+typedef struct revel_replay_stats {
+    uint64_t bytes;            /* bytes replayed */
+    uint64_t windows;          /* windows processed */
+    uint64_t units;            /* physical records (RECORDS) or blocks (FULL_BLOCKS) verified */
+    uint64_t bad;              /* units whose CRC / header failed */
+    uint64_t first_bad_offset; /* file offset of the first bad unit, UINT64_MAX if none */
+    double seconds;            /* host wall time, first read to last verdict */
+    double read_seconds;       /* summed host time spent filling pinned windows */
+    double h2d_ms;             /* summed H2D copy time (HIP events) */
+    double kernel_ms;          /* summed verify time (HIP events) */
+} revel_replay_stats;
+int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t offset, uint64_t length, int mode,
+                          size_t window_bytes, int nbuffers, int io_threads, revel_replay_stats* out);
+int revel_gpu_replay_memory(revel_gpu_context* ctx, const uint8_t* image, uint64_t length, uint64_t base_offset,
+                            int mode, size_t window_bytes, int nbuffers, int io_threads, revel_replay_stats* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,18 @@ class RecordResult(Structure):
 
 assert ctypes.sizeof(RecordResult) == 24
 
+
+class ReplayStats(Structure):
+    _fields_ = [("bytes", c_uint64), ("windows", c_uint64), ("units", c_uint64), ("bad", c_uint64),
+                ("first_bad_offset", c_uint64), ("seconds", ctypes.c_double), ("read_seconds", ctypes.c_double),
+                ("h2d_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+REPLAY_RECORDS, REPLAY_FULL_BLOCKS = 0, 1
+
 # name -> (restype, argtypes); every symbol declared in include/revel_wal.h
 SIGNATURES = {
     "revel_crc32c_value": (c_uint32, [c_void_p, c_size_t]),
@@ -83,6 +95,10 @@ SIGNATURES = {
     "revel_gpu_event_elapsed_ms": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_float)]),
     "revel_gpu_event_free": (c_int, [c_void_p, c_void_p]),
     "revel_last_error": (c_char_p, []),
+    "revel_gpu_replay_file": (c_int, [c_void_p, c_char_p, c_uint64, c_uint64, c_int, c_size_t, c_int, c_int,
+                                      POINTER(ReplayStats)]),
+    "revel_gpu_replay_memory": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_int, c_size_t, c_int, c_int,
+                                        POINTER(ReplayStats)]),
 }
 
 # exported experiment hooks (not part of the public header)

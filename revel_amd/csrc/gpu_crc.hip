@@ -817,6 +817,44 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
 }
 
 // ---------------------------------------------------------------------------
+// Per-window verdict summaries for the end-to-end replay: units, bad units and
+// the smallest bad file offset (summary[0..2]; reset by the host to 0,0,~0).
+// ---------------------------------------------------------------------------
+__global__ void k_summary_records(const revel_record_result* __restrict__ res, const uint32_t* __restrict__ first,
+                                  const uint32_t* __restrict__ counts, uint64_t nblocks,
+                                  unsigned long long* __restrict__ summary) {
+    const uint64_t total = uint64_t(first[nblocks - 1]) + counts[nblocks - 1];
+    unsigned long long bad = 0, first_bad = ~0ull;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (res[i].status != REVEL_REC_OK) {
+            ++bad;
+            first_bad = min(first_bad, (unsigned long long)res[i].file_offset);
+        }
+    }
+    if (bad) {
+        atomicAdd(&summary[1], bad);
+        atomicMin(&summary[2], first_bad);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&summary[0], (unsigned long long)total);
+}
+
+__global__ void k_summary_blocks(const uint8_t* __restrict__ ok, uint64_t nblocks, uint64_t base_offset,
+                                 unsigned long long* __restrict__ summary) {
+    unsigned long long bad = 0, first_bad = ~0ull;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nblocks; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!ok[i]) {
+            ++bad;
+            first_bad = min(first_bad, (unsigned long long)(base_offset + i * kBlockSize));
+        }
+    }
+    if (bad) {
+        atomicAdd(&summary[1], bad);
+        atomicMin(&summary[2], first_bad);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&summary[0], (unsigned long long)nblocks);
+}
+
+// ---------------------------------------------------------------------------
 // Launch helpers
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
@@ -1258,6 +1296,21 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, hipStream_t st) {
     return verify_records_variant(di, 0, d_image, nbytes, base_offset, d_first, d_out, st);
+}
+
+hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
+                             const uint32_t* d_counts, uint64_t nblocks, uint64_t* d_summary, hipStream_t st) {
+    hipLaunchKernelGGL(k_summary_records, dim3((uint32_t)std::max(1, di.num_cu)), dim3(256), 0, st, d_res, d_first,
+                       d_counts, nblocks, reinterpret_cast<unsigned long long*>(d_summary));
+    return hipGetLastError();
+}
+
+hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t nblocks, uint64_t base_offset,
+                            uint64_t* d_summary, hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + 255) / 256));
+    hipLaunchKernelGGL(k_summary_blocks, dim3((uint32_t)grid), dim3(256), 0, st, d_ok, nblocks, base_offset,
+                       reinterpret_cast<unsigned long long*>(d_summary));
+    return hipGetLastError();
 }
 
 }  // namespace revel

@@ -30,6 +30,11 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, hipStream_t st);
 
+hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
+                             const uint32_t* d_counts, uint64_t nblocks, uint64_t* d_summary, hipStream_t st);
+hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t nblocks, uint64_t base_offset,
+                            uint64_t* d_summary, hipStream_t st);
+
 // Set the thread-local error string; returns code.
 int set_error(int code, const char* fmt, ...);
 

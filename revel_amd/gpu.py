@@ -12,7 +12,8 @@ from typing import Optional, Tuple
 
 import numpy as np
 
-from ._lib import BLOCK_SIZE, RecordResult, check, lib
+from ._lib import (BLOCK_SIZE, REPLAY_FULL_BLOCKS, REPLAY_RECORDS, RecordResult, ReplayStats, check,
+                   lib)
 
 RECORD_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("stored_crc", "<u4"),
                          ("computed_crc", "<u4"), ("type", "u1"), ("status", "u1"), ("reserved", "u1", (2,))])
@@ -182,3 +183,21 @@ class GpuContext:
         self.sync()
         res = self.d2h(out, total * RECORD_DTYPE.itemsize, np.uint8).view(RECORD_DTYPE)
         return res
+
+    # ---- end-to-end replay (host -> pinned -> HBM -> verify) ----
+    def replay_memory(self, image, base_offset: int = 0, full_blocks: bool = False, window_bytes: int = 64 << 20,
+                      nbuffers: int = 4, io_threads: int = 8) -> dict:
+        arr = np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray)) else image
+        st = ReplayStats()
+        check(lib().revel_gpu_replay_memory(self._h, arr.ctypes.data, arr.nbytes, base_offset,
+                                            REPLAY_FULL_BLOCKS if full_blocks else REPLAY_RECORDS,
+                                            window_bytes, nbuffers, io_threads, ctypes.byref(st)))
+        return st.as_dict()
+
+    def replay_file(self, path: str, offset: int = 0, length: int = 0, full_blocks: bool = False,
+                    window_bytes: int = 64 << 20, nbuffers: int = 4, io_threads: int = 8) -> dict:
+        st = ReplayStats()
+        check(lib().revel_gpu_replay_file(self._h, path.encode(), offset, length,
+                                          REPLAY_FULL_BLOCKS if full_blocks else REPLAY_RECORDS,
+                                          window_bytes, nbuffers, io_threads, ctypes.byref(st)))
+        return st.as_dict()
