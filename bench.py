@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound on the CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
+    ap.add_argument("--e2e-gib", type=float, default=4.0,
+                    help="per-rank host-RAM replay size for the end_to_end field (0 = skip)")
     return ap.parse_args()
 
 
@@ -142,6 +144,31 @@ def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
     }
 
 
+def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
+    """PCIe-inclusive rate (not `value`): every rank replays `gib` GiB of its
+    blocks from a pageable host-RAM image through the pinned ring -> H2D ->
+    verify pipeline (revel_gpu_replay_memory), all ranks started together;
+    rate = total bytes / max-over-ranks wall time."""
+    k = min(nblocks, int(gib * (1 << 30)) // BLOCK_SIZE)
+    host = ctx.d2h(dblocks, k * BLOCK_SIZE)              # host image = the first k device blocks
+    D.barrier()
+    t0 = time.perf_counter()
+    st = ctx.replay_memory(host, full_blocks=True, window_bytes=64 << 20, nbuffers=4, io_threads=8)
+    wall = time.perf_counter() - t0
+    D.barrier()
+    wall_max = D.max(wall)
+    bad = D.sum(float(st["bad"]))
+    return {
+        "unit": "GiB/s",
+        "value": round(k * BLOCK_SIZE * D.world / 2**30 / wall_max, 2),
+        "per_rank_GiB": round(k * BLOCK_SIZE / 2**30, 2),
+        "h2d_GiB_s_rank0": round(k * BLOCK_SIZE / 2**30 / (st["h2d_ms"] / 1e3), 2),
+        "bad_blocks": int(bad),
+        "path": "pageable host RAM -> 8 memcpy threads -> 4 x 64 MiB pinned ring -> H2D (copy stream) -> "
+                "C2 verify (compute stream) -> 24 B summary D2H per window",
+    }
+
+
 def main():
     args = parse()
     D = Dist()
@@ -187,6 +214,10 @@ def main():
     achieved = alg_bytes / (kern_ms_max / 1e3) / 1e9
     traffic = pmc_traffic(n)
 
+    e2e = None
+    if args.e2e_gib > 0:
+        e2e = end_to_end(ctx, D, dblocks, n, args.e2e_gib)
+
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(ctx, dblocks, masked, n, args.cpu_seconds)
@@ -225,6 +256,7 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
             },
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
         }
         print(json.dumps(out), flush=True)
     D.close()
