@@ -130,6 +130,7 @@ def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
         got = oracle_c.full_block_crcs(sample, v)
         ctxt[v] = round(len(idx) * BLOCK_SIZE / 2**30 / (time.perf_counter() - t0), 3)
         parity = parity and bool(np.array_equal(got, gpu_crc))
+    c1 = c1_reference_path(oracle_c)
     return {
         "value": round(done * BLOCK_SIZE / 2**30 / t_byte, 4),
         "unit": "GiB/s",
@@ -141,7 +142,29 @@ def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
         "context_GiB_s_1core": ctxt,
         "host_cores_available": os.cpu_count(),
         "parity_vs_gpu": parity,
+        "c1_reference_path": c1,
     }
+
+
+def c1_reference_path(oracle_c):
+    """Config C1 on the CPU: 10 000 x 4 KiB records appended with the oracle's
+    writer restatement (log_writer.rs:58-124, bytewise CRC) and read back with
+    its per-record CRC walk (log_reader.rs:200-206 made per record), one thread."""
+    from oracle import crc32c_oracle as po
+    words = po.splitmix64_np(np.uint64(0x5EED0001) ^ np.arange(10000, dtype=np.uint64), 512)
+    recs = [words[i].tobytes() for i in range(10000)]
+    t0 = time.perf_counter()
+    image = oracle_c.write_image(recs)
+    t_w = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    walk = oracle_c.walk(image)
+    t_r = time.perf_counter() - t0
+    ok = bool((walk["status"] == 0).all()) and len(image) == 41038750
+    mb = 10000 * 4096 / 1e6
+    return {"records": 10000, "record_bytes": 4096, "image_bytes": len(image), "all_crc_ok": ok,
+            "append_records_per_s": round(10000 / t_w), "append_MB_s": round(mb / t_w, 1),
+            "readback_verify_records_per_s": round(10000 / t_r), "readback_verify_MB_s": round(mb / t_r, 1),
+            "note": "reference's own reader cannot complete C1 (SURVEY App. A #1-3); LevelDB-correct walk timed"}
 
 
 def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
