@@ -179,6 +179,23 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
                              uint64_t base_offset, const uint32_t* d_first,
                              revel_record_result* d_out, void* stream);
 
+/* ---- device append framing (log_writer.rs:58-124 for a whole batch) ----- */
+/* Bytes that n successive add_record calls starting at block_offset would
+ * append (headers, payloads, zero trailers). */
+uint64_t revel_log_framed_size(const uint64_t* lens, size_t n, uint64_t block_offset);
+/* Frame n records on the GPU exactly as n successive
+ * Writer::add_record calls would (log_writer.rs:58-97): payloads are
+ * concatenated in device memory (d_payloads), lengths on the host.  The
+ * fragment layout is computed on the host; payload scatter, zero trailers and
+ * every header's masked CRC32C are computed on the device.  The image (the
+ * bytes the writer would append, starting at *block_offset within the current
+ * block) goes to d_image (capacity image_cap); *image_len receives its size
+ * and *block_offset is advanced like Writer::block_offset.  Returns when the
+ * image is complete. */
+int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, const uint64_t* lens, size_t n,
+                             uint64_t* block_offset, void* d_image, size_t image_cap, size_t* image_len,
+                             void* stream);
+
 /* ---- device plumbing (used by the reader, tests and bench) -------------- */
 int revel_gpu_malloc(revel_gpu_context* ctx, size_t n, void** d_ptr);
 int revel_gpu_free(revel_gpu_context* ctx, void* d_ptr);

@@ -95,6 +95,9 @@ SIGNATURES = {
     "revel_gpu_event_elapsed_ms": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_float)]),
     "revel_gpu_event_free": (c_int, [c_void_p, c_void_p]),
     "revel_last_error": (c_char_p, []),
+    "revel_log_framed_size": (c_uint64, [c_void_p, c_size_t, c_uint64]),
+    "revel_gpu_append_records": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_uint64), c_void_p,
+                                         c_size_t, POINTER(c_size_t), c_void_p]),
     "revel_gpu_replay_file": (c_int, [c_void_p, c_char_p, c_uint64, c_uint64, c_int, c_size_t, c_int, c_int,
                                       POINTER(ReplayStats)]),
     "revel_gpu_replay_memory": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_int, c_size_t, c_int, c_int,

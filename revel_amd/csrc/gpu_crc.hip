@@ -399,6 +399,28 @@ __device__ __forceinline__ Hdr read_header(const uint8_t* base, uint32_t off, ui
     return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
 }
 
+// 16 bytes at block offset pos, zero outside [lo, bl) (lo > 0 only for the
+// first block of an image that starts mid-block).
+__device__ __forceinline__ uint4 load16_range(const uint8_t* blk, uint32_t pos, uint32_t lo, uint32_t bl) {
+    if (pos >= lo && pos + 16u <= bl) return ldg4_plain(reinterpret_cast<const uint4*>(blk + pos));
+    uint8_t t[16];
+    for (uint32_t k = 0; k < 16; ++k) t[k] = (pos + k >= lo && pos + k < bl) ? blk[pos + k] : 0;
+    uint4 v;
+    memcpy(&v, t, 16);
+    return v;
+}
+
+__device__ __forceinline__ Hdr read_header_range(const uint8_t* base, uint32_t off, uint32_t lo, uint32_t bl) {
+    if ((off & ~3u) >= lo) return read_header(base, off, bl);
+    uint8_t t[8];
+    for (uint32_t k = 0; k < 7; ++k) t[k] = base[off + k];  // off >= lo, off + 7 <= bl
+    t[7] = 0;
+    uint32_t a, b;
+    memcpy(&a, t, 4);
+    memcpy(&b, t + 4, 4);
+    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
+}
+
 // 16 bytes at block offset pos, zero past bl.
 __device__ __forceinline__ uint4 load16_guarded(const uint8_t* blk, uint32_t pos, uint32_t bl) {
     if (pos + 16u <= bl) return ldg4(reinterpret_cast<const uint4*>(blk + pos));
@@ -666,10 +688,16 @@ __device__ __forceinline__ uint32_t byte_step_s4r(uint32_t state, uint32_t b, La
     return ldsw<128>(tab, a) ^ (state >> 8);
 }
 
+// FRAME = device append framing: headers hold length/type but no CRC yet;
+// the kernel writes mask(crc32c(type||payload)) into bytes [off, off+4) of
+// each header instead of emitting result records.  `lead` = in-block offset
+// of image byte 0 (a batch appended to a partially written block).
+template <bool FRAME>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
-                                                                     revel_record_result* __restrict__ out) {
+                                                                     revel_record_result* __restrict__ out,
+                                                                     uint32_t lead) {
     __shared__ uint32_t tab[32768];
     __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
     fill_tables<TM_S4R>(tab);
@@ -677,26 +705,28 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
     VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
     const LaneConst L = make_lane_const();
     const uint32_t lane = lane_id();
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t vbytes = nbytes + lead;  // bytes of the virtual block-aligned image
+    const uint64_t nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
     const uint64_t waves_per_wg = kVerify2Threads / 64;
     const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
     const uint64_t nwaves = gridDim.x * waves_per_wg;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
 
     for (uint64_t b = gwave; b < nblocks; b += nwaves) {
-        const uint64_t base = b * kBlockSize;
-        const uint8_t* blk = image + base;
-        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
-        const bool full = bl == kBlockSize;
+        const uint64_t base = b * kBlockSize;  // virtual offset of the block
+        const uint8_t* blk = image + base - lead;  // dereferenced only at [lo, bl)
+        const uint32_t lo_b = b == 0 ? lead : 0u;
+        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, vbytes - base);
+        const bool full = bl == kBlockSize && lo_b == 0;
         const uint32_t cs = lane * 512u, ce = cs + 512u;
-        uint32_t out_base = first[b];
-        uint32_t walk_from = 0;
+        uint32_t out_base = FRAME ? 0u : first[b];
+        uint32_t walk_from = lo_b;
         for (;;) {
             if (lane == 0) {
                 uint32_t off = walk_from, n = 0, cont = kNone;
                 while (bl - off >= kHeaderSize) {
                     if (n == kRecCap2) { cont = off; break; }
-                    const Hdr h = read_header(blk, off, bl);
+                    const Hdr h = read_header_range(blk, off, lo_b, bl);
                     const uint32_t st = classify(h, off, bl);
                     wl.s[n] = (uint16_t)(off + 6);
                     wl.em1[n] = (uint16_t)(st == REVEL_REC_OK ? off + kHeaderSize + h.len - 1u : off + 5u);
@@ -733,7 +763,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                     for (int j = 0; j < 8; ++j) {
                         const uint32_t pos = cs + rr * 128 + j * 16;
                         v[j] = full ? ldg4_plain(reinterpret_cast<const uint4*>(blk + pos))
-                                    : (pos < bl ? load16_guarded(blk, pos, bl) : make_uint4(0, 0, 0, 0));
+                                    : (pos < bl ? load16_range(blk, pos, lo_b, bl) : make_uint4(0, 0, 0, 0));
                     }
                 };
                 uint4 cur[8], nxt[8];
@@ -791,27 +821,68 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
             wave_lds_sync();
             for (uint32_t k = lane; k < nrec; k += 64) {
                 const uint32_t off = uint32_t(wl.s[k]) - 6u;
-                const Hdr h = read_header(blk, off, bl);
+                const Hdr h = read_header_range(blk, off, lo_b, bl);
                 const uint32_t st = classify(h, off, bl);
-                revel_record_result res;
-                res.file_offset = base_offset + base + off;
-                res.length = h.len;
-                res.stored_crc = h.stored;
-                res.type = (uint8_t)h.type;
-                res.reserved[0] = res.reserved[1] = 0;
-                if (st == REVEL_REC_OK) {
-                    res.computed_crc = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
-                    res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
+                if constexpr (FRAME) {
+                    if (st == REVEL_REC_OK) {
+                        const uint32_t m = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                        uint8_t* hp = const_cast<uint8_t*>(blk) + off;
+                        hp[0] = (uint8_t)m;
+                        hp[1] = (uint8_t)(m >> 8);
+                        hp[2] = (uint8_t)(m >> 16);
+                        hp[3] = (uint8_t)(m >> 24);
+                    }
                 } else {
-                    res.computed_crc = 0;
-                    res.status = (uint8_t)st;
+                    revel_record_result res;
+                    res.file_offset = base_offset + base - lead + off;
+                    res.length = h.len;
+                    res.stored_crc = h.stored;
+                    res.type = (uint8_t)h.type;
+                    res.reserved[0] = res.reserved[1] = 0;
+                    if (st == REVEL_REC_OK) {
+                        res.computed_crc = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                        res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
+                    } else {
+                        res.computed_crc = 0;
+                        res.status = (uint8_t)st;
+                    }
+                    out[out_base + k] = res;
                 }
-                out[out_base + k] = res;
             }
             out_base += nrec;
             wave_lds_sync();
             if (cont == kNone) break;
             walk_from = cont;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Device append framing, step 1: scatter fragments (payload bytes + length
+// and type header bytes, CRC left zero) and zero the block trailers.  One
+// wave per fragment; the layout comes from the host (frame_layout()).
+// ---------------------------------------------------------------------------
+__global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const revel::FragDesc* __restrict__ frags,
+                                    uint64_t nfrags, uint8_t* __restrict__ image) {
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t f = blockIdx.x * (uint64_t)(blockDim.x / 64) + (threadIdx.x >> 6); f < nfrags; f += waves) {
+        const revel::FragDesc d = frags[f];
+        uint8_t* dst = image + d.dst;
+        const uint32_t lane = lane_id();
+        if (d.type == revel::kTrailer) {
+            for (uint32_t i = lane; i < d.len; i += 64) dst[i] = 0;
+            continue;
+        }
+        if (lane < 7) {
+            const uint8_t hv[7] = {0, 0, 0, 0, (uint8_t)(d.len & 0xffu), (uint8_t)(d.len >> 8), (uint8_t)d.type};
+            dst[lane] = hv[lane];
+        }
+        const uint8_t* src = payloads + d.src;
+        uint8_t* pd = dst + kHeaderSize;
+        for (uint32_t i = lane * 4; i < d.len; i += 256) {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+                if (i + k < d.len) pd[i + k] = src[i + k];
         }
     }
 }
@@ -1267,6 +1338,18 @@ hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t*
     return hipGetLastError();
 }
 
+// One-time per device (per thread): the x^(8d) / init_xor(d) tables.
+static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
+    static thread_local int inited_dev = -1;
+    if (inited_dev != di.device) {
+        hipLaunchKernelGGL(k_init_len_tables, dim3(64), dim3(256), 0, st);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        inited_dev = di.device;
+    }
+    return hipSuccess;
+}
+
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                   hipStream_t st) {
@@ -1279,17 +1362,12 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
                            static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out);
         return hipGetLastError();
     }
-    static thread_local int inited_dev = -1;
-    if (inited_dev != di.device) {  // one-time per device (per thread): x^(8d), init_xor(d) tables
-        hipLaunchKernelGGL(k_init_len_tables, dim3(64), dim3(256), 0, st);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        inited_dev = di.device;
-    }
+    hipError_t e0 = ensure_len_tables(di, st);
+    if (e0 != hipSuccess) return e0;
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
-    hipLaunchKernelGGL(k_verify_records2, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out);
+    hipLaunchKernelGGL(k_verify_records2<false>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out, 0u);
     return hipGetLastError();
 }
 
@@ -1310,6 +1388,26 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + 255) / 256));
     hipLaunchKernelGGL(k_summary_blocks, dim3((uint32_t)grid), dim3(256), 0, st, d_ok, nblocks, base_offset,
                        reinterpret_cast<unsigned long long*>(d_summary));
+    return hipGetLastError();
+}
+
+hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
+                         void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st) {
+    if (nfrags) {
+        const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (nfrags + 3) / 4));
+        hipLaunchKernelGGL(k_scatter_fragments, dim3((uint32_t)grid), dim3(256), 0, st,
+                           static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image));
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (image_len == 0) return hipSuccess;
+    hipError_t e = ensure_len_tables(di, st);
+    if (e != hipSuccess) return e;
+    const uint64_t nblocks = (image_len + lead + kBlockSize - 1) / kBlockSize;
+    const uint64_t waves = kVerify2Threads / 64;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
+    hipLaunchKernelGGL(k_verify_records2<true>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
+                       static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr, lead);
     return hipGetLastError();
 }
 

@@ -8,6 +8,16 @@
 
 namespace revel {
 
+// One physical record (or a zero trailer) of a batch append, laid out on the
+// host by frame_layout() exactly as log_writer.rs:58-97 would.
+constexpr uint32_t kTrailer = 0xFFu;
+struct FragDesc {
+    uint64_t dst;  // image offset of the 7-byte header (or of the trailer)
+    uint64_t src;  // payload offset
+    uint32_t len;  // payload length (trailer length for kTrailer)
+    uint32_t type;  // record type, or kTrailer
+};
+
 struct DeviceInfo {
     int device = 0;
     int num_cu = 256;
@@ -34,6 +44,9 @@ hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_
                              const uint32_t* d_counts, uint64_t nblocks, uint64_t* d_summary, hipStream_t st);
 hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t nblocks, uint64_t base_offset,
                             uint64_t* d_summary, hipStream_t st);
+
+hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
+                         void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st);
 
 // Set the thread-local error string; returns code.
 int set_error(int code, const char* fmt, ...);

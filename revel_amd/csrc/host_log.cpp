@@ -331,6 +331,88 @@ int revel_log_writer_add_record(revel_log_writer* w, const uint8_t* data, size_t
 
 uint64_t revel_log_writer_block_offset(const revel_log_writer* w) { return w ? w->block_offset : 0; }
 
+}  // extern "C"
+
+// Fragment layout of a batch of records (log_writer.rs:58-97, as the host
+// writer above), for device append framing.
+namespace {
+
+uint64_t frame_layout(const uint64_t* lens, size_t n, uint64_t& boff, std::vector<revel::FragDesc>* frags) {
+    uint64_t pos = 0, src = 0;
+    for (size_t r = 0; r < n; ++r) {
+        uint64_t left = lens[r], off = 0;
+        bool begin = true;
+        for (;;) {
+            const uint64_t leftover = REVEL_BLOCK_SIZE - boff;
+            if (leftover < REVEL_HEADER_SIZE) {
+                if (leftover > 0) {
+                    if (frags) frags->push_back({pos, 0, (uint32_t)leftover, revel::kTrailer});
+                    pos += leftover;
+                }
+                boff = 0;
+            }
+            const uint64_t avail = REVEL_BLOCK_SIZE - boff - REVEL_HEADER_SIZE;
+            const uint64_t frag = left < avail ? left : avail;
+            const bool end = left == frag;
+            const uint32_t type = (begin && end) ? REVEL_FULL_TYPE
+                                  : begin        ? REVEL_FIRST_TYPE
+                                  : end          ? REVEL_LAST_TYPE
+                                                 : REVEL_MIDDLE_TYPE;
+            if (frags) frags->push_back({pos, src + off, (uint32_t)frag, type});
+            pos += REVEL_HEADER_SIZE + frag;
+            boff += REVEL_HEADER_SIZE + frag;
+            off += frag;
+            left -= frag;
+            begin = false;
+            if (left == 0) break;
+        }
+        src += lens[r];
+    }
+    return pos;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t revel_log_framed_size(const uint64_t* lens, size_t n, uint64_t block_offset) {
+    if ((!lens && n) || block_offset > REVEL_BLOCK_SIZE) return 0;
+    uint64_t boff = block_offset;
+    return frame_layout(lens, n, boff, nullptr);
+}
+
+int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, const uint64_t* lens, size_t n,
+                             uint64_t* block_offset, void* d_image, size_t image_cap, size_t* image_len,
+                             void* stream) {
+    if (!ctx || !block_offset || !image_len || (!lens && n)) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
+    if (*block_offset > REVEL_BLOCK_SIZE)
+        return set_error(REVEL_INVALID_ARGUMENT, "block_offset %llu > block size", (unsigned long long)*block_offset);
+    uint64_t boff = *block_offset;
+    const uint32_t lead = (uint32_t)(boff % REVEL_BLOCK_SIZE);
+    std::vector<revel::FragDesc> frags;
+    const uint64_t len = frame_layout(lens, n, boff, &frags);
+    *image_len = 0;
+    if (len > image_cap) return set_error(REVEL_INVALID_ARGUMENT, "image capacity %zu < %llu", image_cap,
+                                          (unsigned long long)len);
+    if (len && (!d_image || (!d_payloads && frags.size()))) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    revel::FragDesc* d_frags = nullptr;
+    hipError_t e = hipSuccess;
+    if (!frags.empty()) {
+        e = hipMalloc(reinterpret_cast<void**>(&d_frags), frags.size() * sizeof(revel::FragDesc));
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_frags, frags.data(), frags.size() * sizeof(revel::FragDesc), hipMemcpyHostToDevice, st);
+    }
+    if (e == hipSuccess) e = revel::frame_records(ctx->di, d_payloads, d_frags, frags.size(), d_image, len, lead, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (d_frags) (void)hipFree(d_frags);
+    if (e != hipSuccess) return set_error(REVEL_IO_ERROR, "append_records: %s", hipGetErrorString(e));
+    *image_len = len;
+    *block_offset = boff;
+    return REVEL_OK;
+}
+
 void revel_log_writer_free(revel_log_writer* w) { delete w; }
 
 }  // extern "C"

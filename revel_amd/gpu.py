@@ -201,3 +201,17 @@ class GpuContext:
                                           REPLAY_FULL_BLOCKS if full_blocks else REPLAY_RECORDS,
                                           window_bytes, nbuffers, io_threads, ctypes.byref(st)))
         return st.as_dict()
+
+    # ---- device append framing (batch add_record) ----
+    def append_records(self, payloads: DeviceBuffer, lens, block_offset: int = 0):
+        """Frame records on the GPU as successive Writer.add_record calls
+        would; returns (image DeviceBuffer, image_len, new block_offset)."""
+        lens = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        L = lib()
+        size = L.revel_log_framed_size(lens.ctypes.data, len(lens), block_offset)
+        img = self.alloc(max(1, size))
+        bo = ctypes.c_uint64(block_offset)
+        n = ctypes.c_size_t()
+        check(L.revel_gpu_append_records(self._h, payloads.ptr, lens.ctypes.data, len(lens), ctypes.byref(bo),
+                                         img.ptr, img.nbytes, ctypes.byref(n), None))
+        return img, n.value, bo.value

@@ -282,3 +282,35 @@ def test_replay_full_blocks_and_file(gpu_ctx, tmp_path):
     # records mode on the same file: every block is one FULL record
     st = gpu_ctx.replay_file(path, offset=100 * BLOCK_SIZE, window_bytes=64 * BLOCK_SIZE, io_threads=2)
     assert (st["units"], st["bad"], st["first_bad_offset"]) == (200, 2, 123 * BLOCK_SIZE)
+
+
+# ---- device append framing (batch add_record) vs the oracle writer ----
+@pytest.mark.parametrize("block_offset", [0, 1, 6, 7, 100, 32760, 32761, 32762, 32767, 32768])
+def test_append_records_matches_writer(gpu_ctx, block_offset):
+    rng = np.random.default_rng(block_offset + 1)
+    sizes = list(rng.integers(0, 3000, 40)) + [0, 0, 32761, 32754, 70000, 1, 5] + list(rng.integers(0, 100, 300))
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    blob = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    d = gpu_ctx.upload(blob if blob.size else np.zeros(1, np.uint8))
+    img, n, bo = gpu_ctx.append_records(d, [len(r) for r in recs], block_offset)
+    want = oc.write_image(recs, block_offset)
+    w = po.LogWriter(block_offset=block_offset)
+    for r in recs:
+        w.add_record(r)
+    assert bo == w.block_offset
+    assert n == len(want)
+    assert gpu_ctx.d2h(img, n).tobytes() == want
+
+
+def test_append_records_c1_and_readback(gpu_ctx):
+    words = po.splitmix64_np(np.uint64(0x5EED0001) ^ np.arange(10000, dtype=np.uint64), 512)
+    d = gpu_ctx.upload(words.view(np.uint8).ravel())
+    img, n, bo = gpu_ctx.append_records(d, [4096] * 10000, 0)
+    assert n == 41038750
+    host = gpu_ctx.d2h(img, n).tobytes()
+    import hashlib
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_records.npz"))
+    assert hashlib.sha256(host).digest() == z["sha256"].tobytes()
+    res = gpu_ctx.verify_image(img, n)
+    assert len(res) == 11250 and (res["status"] == 0).all()

@@ -170,3 +170,13 @@ def test_reader_initial_offset():
         got = list(rd)
         want = po.read_all(img, checksum=False, initial_offset=off)
         assert got == want, off
+
+
+def test_framed_size_matches_writer():
+    import ctypes
+    rng = np.random.default_rng(9)
+    for boff in [0, 1, 7, 32760, 32762, 32768]:
+        recs = [b"x" * int(s) for s in rng.integers(0, 70000, 30)] + [b""] * 5
+        lens = np.array([len(r) for r in recs], dtype=np.uint64)
+        n = revel_amd.lib().revel_log_framed_size(lens.ctypes.data, len(lens), boff)
+        assert n == len(po.write_image(recs, boff))
