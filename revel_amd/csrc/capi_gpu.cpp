@@ -115,6 +115,7 @@ void revel_gpu_context_free(revel_gpu_context* ctx) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamDestroy(ctx->stream);
     }
+    if (ctx->hlist) (void)hipFree(ctx->hlist);
     delete ctx;
 }
 
@@ -164,7 +165,20 @@ int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t 
     CHECK_CTX(ctx);
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_counts) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, pick(ctx, stream)), "count_records launch");
+    const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
+    if (nblocks > ctx->hlist_cap_blocks) {
+        if (ctx->hlist) (void)hipFree(ctx->hlist);
+        ctx->hlist = nullptr;
+        ctx->hlist_cap_blocks = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->hlist), nblocks * revel::kListPerBlock * sizeof(uint32_t)),
+                "hipMalloc(header list)");
+        ctx->hlist_cap_blocks = nblocks;
+    }
+    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, ctx->hlist, pick(ctx, stream)),
+            "count_records launch");
+    ctx->hlist_image = d_image;
+    ctx->hlist_nbytes = nbytes;
+    ctx->hlist_counts = d_counts;
     return REVEL_OK;
 }
 
@@ -182,8 +196,11 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     CHECK_CTX(ctx);
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    HIP_TRY(revel::verify_records(ctx->di, d_image, nbytes, base_offset, d_first, d_out, pick(ctx, stream)),
+    const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
+    HIP_TRY(revel::verify_records(ctx->di, d_image, nbytes, base_offset, d_first, d_out, memo ? ctx->hlist : nullptr,
+                                  memo ? ctx->hlist_counts : nullptr, pick(ctx, stream)),
             "verify_records launch");
+    ctx->hlist_image = nullptr;  // one count pass -> one verify
     return REVEL_OK;
 }
 
@@ -194,9 +211,12 @@ int revel_gpu_verify_records_variant(revel_gpu_context* ctx, int variant, const 
     CHECK_CTX(ctx);
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
     HIP_TRY(revel::verify_records_variant(ctx->di, variant, d_image, nbytes, base_offset, d_first, d_out,
+                                          memo ? ctx->hlist : nullptr, memo ? ctx->hlist_counts : nullptr,
                                           pick(ctx, stream)),
             "verify_records_variant launch");
+    ctx->hlist_image = nullptr;
     return REVEL_OK;
 }
 

@@ -438,7 +438,11 @@ __device__ __forceinline__ uint32_t classify(const Hdr& h, uint32_t off, uint32_
     return REVEL_REC_OK;
 }
 
-__global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts) {
+// Per block (one lane each): number of physical records and, when list is
+// non-null, the first kListPerBlock headers as (offset | len << 16), len =
+// 0xFFFF marking a bad header (zero record / length past the block).
+__global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts,
+                                uint32_t* __restrict__ hlist) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
          b += (uint64_t)gridDim.x * blockDim.x) {
@@ -448,8 +452,10 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
         uint32_t off = 0, n = 0;
         while (bl - off >= kHeaderSize) {
             const Hdr h = read_header(blk, off, bl);
+            const bool ok = classify(h, off, bl) == REVEL_REC_OK;
+            if (hlist && n < kListPerBlock) hlist[b * kListPerBlock + n] = off | ((ok ? h.len : 0xFFFFu) << 16);
             ++n;
-            if (classify(h, off, bl) != REVEL_REC_OK) break;
+            if (!ok) break;
             off += kHeaderSize + h.len;
         }
         counts[b] = n;
@@ -660,7 +666,7 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify_records(const uint8_t
 // path, exact tails.
 // ---------------------------------------------------------------------------
 constexpr int kVerify2Threads = 1024;
-constexpr uint32_t kRecCap2 = 128;
+constexpr uint32_t kRecCap2 = 128;  // >= kListPerBlock
 
 // x^(8d) and init_xor(d) for d = 0..32768, filled once per device.
 __device__ uint32_t g_x8n_tab[kBlockSize + 1];
@@ -697,7 +703,9 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
                                                                      revel_record_result* __restrict__ out,
-                                                                     uint32_t lead) {
+                                                                     uint32_t lead,
+                                                                     const uint32_t* __restrict__ hlist,
+                                                                     const uint32_t* __restrict__ counts) {
     __shared__ uint32_t tab[32768];
     __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
     fill_tables<TM_S4R>(tab);
@@ -721,8 +729,35 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
         const uint32_t cs = lane * 512u, ce = cs + 512u;
         uint32_t out_base = FRAME ? 0u : first[b];
         uint32_t walk_from = lo_b;
+        auto load_round = [&](uint4* v, int rr) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t pos = cs + rr * 128 + j * 16;
+                v[j] = full ? ldg4_plain(reinterpret_cast<const uint4*>(blk + pos))
+                            : (pos < bl ? load16_range(blk, pos, lo_b, bl) : make_uint4(0, 0, 0, 0));
+            }
+        };
+        // the chunk's first round does not depend on the record list: issue it now
+        uint4 cur[8], nxt[8];
+        load_round(cur, 0);
+        bool have_round0 = true;
+        // header list from the count pass (parallel per-block walks) when it
+        // covers the whole block; otherwise lane 0 walks here.
+        const uint32_t nlist = (hlist && counts) ? counts[b] : kNone;
         for (;;) {
-            if (lane == 0) {
+            if (walk_from == lo_b && nlist <= kListPerBlock) {
+                for (uint32_t k = lane; k < nlist; k += 64) {
+                    const uint32_t e = hlist[b * kListPerBlock + k];
+                    const uint32_t off = e & 0xFFFFu, len = e >> 16;
+                    wl.s[k] = (uint16_t)(off + 6);
+                    wl.em1[k] = (uint16_t)(len == 0xFFFFu ? off + 5u : off + kHeaderSize + len - 1u);
+                    wl.acc[k] = 0;
+                }
+                if (lane == 0) {
+                    wl.nrec = nlist;
+                    wl.more_off = kNone;
+                }
+            } else if (lane == 0) {
                 uint32_t off = walk_from, n = 0, cont = kNone;
                 while (bl - off >= kHeaderSize) {
                     if (n == kRecCap2) { cont = off; break; }
@@ -754,20 +789,10 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
             uint32_t r = lo, s, e;
             load_rec(r, s, e);
             while (r < nrec && s == e) { ++r; load_rec(r, s, e); }
-            const uint32_t rec_lo = __builtin_amdgcn_readfirstlane(lo);
             const bool active = cs < bl && r < nrec && s < ce;
             uint32_t state = 0;
             if (__any(active)) {
-                auto load_round = [&](uint4* v, int rr) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const uint32_t pos = cs + rr * 128 + j * 16;
-                        v[j] = full ? ldg4_plain(reinterpret_cast<const uint4*>(blk + pos))
-                                    : (pos < bl ? load16_range(blk, pos, lo_b, bl) : make_uint4(0, 0, 0, 0));
-                    }
-                };
-                uint4 cur[8], nxt[8];
-                load_round(cur, 0);
+                if (!have_round0) load_round(cur, 0);
 #pragma unroll 1
                 for (int rr = 0; rr < 4; ++rr) {
                     if (rr < 3) load_round(nxt, rr + 1);
@@ -817,7 +842,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                 // record still open at the chunk end: shift its partial register to e
                 if (cs < bl && r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[e - ce], state));
             }
-            (void)rec_lo;
+            have_round0 = false;
             wave_lds_sync();
             for (uint32_t k = lane; k < nrec; k += 64) {
                 const uint32_t off = uint32_t(wl.s[k]) - 6u;
@@ -1325,11 +1350,11 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 }
 
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                         hipStream_t st) {
+                         uint32_t* d_hlist, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 4, (nblocks + 63) / 64));
     hipLaunchKernelGGL(k_count_records, dim3((uint32_t)grid), dim3(64), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, d_counts);
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist);
     return hipGetLastError();
 }
 
@@ -1352,7 +1377,7 @@ static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
 
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                  hipStream_t st) {
+                                  const uint32_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (variant == 1) {
         const uint64_t waves = kVerifyThreads / 64;
@@ -1367,13 +1392,15 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     hipLaunchKernelGGL(k_verify_records2<false>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out, 0u);
+                       static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out, 0u,
+                       variant == 2 ? nullptr : d_hlist, d_counts);
     return hipGetLastError();
 }
 
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                          const uint32_t* d_first, revel_record_result* d_out, hipStream_t st) {
-    return verify_records_variant(di, 0, d_image, nbytes, base_offset, d_first, d_out, st);
+                          const uint32_t* d_first, revel_record_result* d_out, const uint32_t* d_hlist,
+                          const uint32_t* d_counts, hipStream_t st) {
+    return verify_records_variant(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
 }
 
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
@@ -1407,7 +1434,7 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     hipLaunchKernelGGL(k_verify_records2<true>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr, lead);
+                       static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr, lead, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--variants", default="0,2,1")
     a = ap.parse_args()
     t0 = time.time()
     img = make_image(a.bytes)
