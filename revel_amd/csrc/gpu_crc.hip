@@ -462,32 +462,32 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 
-// Exclusive scan, one workgroup of 1024 threads, sequential 1024-chunks.
+// Exclusive scan, one workgroup of 1024 threads: thread t owns the
+// contiguous segment [t*seg, (t+1)*seg); segment sums are scanned across the
+// workgroup (wave shuffles + LDS), then each thread writes its segment.
 __global__ __launch_bounds__(1024) void k_exclusive_scan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                         uint64_t n) {
     __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry_s;
-    if (threadIdx.x == 0) carry_s = 0;
-    __syncthreads();
-    for (uint64_t base = 0; base < n; base += 1024) {
-        const uint64_t i = base + threadIdx.x;
-        const uint32_t v = i < n ? in[i] : 0u;
-        uint32_t x = v;
+    const uint64_t seg = (n + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * seg, hi = std::min<uint64_t>(n, lo + seg);
+    uint32_t sum = 0;
+    for (uint64_t i = lo; i < hi; ++i) sum += in[i];
+    uint32_t x = sum;  // inclusive scan of segment sums inside the wave
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if ((int)lane_id() >= d) x += y;
-        }
-        const uint32_t w = threadIdx.x >> 6;
-        if (lane_id() == 63) wsum[w] = x;
-        __syncthreads();
-        uint32_t woff = 0;
-        for (uint32_t k = 0; k < w; ++k) woff += wsum[k];
-        const uint32_t carry = carry_s;
-        if (i < n) out[i] = carry + woff + x - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry_s = carry + woff + x;
-        __syncthreads();
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if ((int)lane_id() >= d) x += y;
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane_id() == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < w; ++k) run += wsum[k];
+    run += x - sum;  // exclusive prefix of this thread's segment
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t v = in[i];
+        out[i] = run;
+        run += v;
     }
 }
 
