@@ -116,6 +116,7 @@ void revel_gpu_context_free(revel_gpu_context* ctx) {
         (void)hipStreamDestroy(ctx->stream);
     }
     if (ctx->hlist) (void)hipFree(ctx->hlist);
+    if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
     delete ctx;
 }
 
@@ -187,7 +188,15 @@ int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, u
     CHECK_CTX(ctx);
     if (n == 0) return REVEL_OK;
     if (!d_in || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    HIP_TRY(revel::exclusive_scan_u32(ctx->di, d_in, d_out, n, pick(ctx, stream)), "scan launch");
+    const uint64_t words = revel::scan_scratch_words(n);
+    if (words > ctx->scan_scratch_cap) {
+        if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
+        ctx->scan_scratch = nullptr;
+        ctx->scan_scratch_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->scan_scratch), words * sizeof(uint32_t)), "hipMalloc(scan)");
+        ctx->scan_scratch_cap = words;
+    }
+    HIP_TRY(revel::exclusive_scan_u32(ctx->di, d_in, d_out, n, ctx->scan_scratch, pick(ctx, stream)), "scan launch");
     return REVEL_OK;
 }
 

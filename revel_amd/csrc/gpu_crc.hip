@@ -462,17 +462,53 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 
-// Exclusive scan, one workgroup of 1024 threads: thread t owns the
-// contiguous segment [t*seg, (t+1)*seg); segment sums are scanned across the
-// workgroup (wave shuffles + LDS), then each thread writes its segment.
-__global__ __launch_bounds__(1024) void k_exclusive_scan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                        uint64_t n) {
-    __shared__ uint32_t wsum[16];
-    const uint64_t seg = (n + 1023) / 1024;
-    const uint64_t lo = threadIdx.x * seg, hi = std::min<uint64_t>(n, lo + seg);
-    uint32_t sum = 0;
-    for (uint64_t i = lo; i < hi; ++i) sum += in[i];
-    uint32_t x = sum;  // inclusive scan of segment sums inside the wave
+// Exclusive scan in two parallel passes over tiles of kScanTile elements
+// (256 threads x 4): k_tile_sums writes each tile's sum; k_scan_apply adds the
+// sums of the tiles before it and scans its own tile.
+constexpr uint32_t kScanTile = 1024;
+
+__device__ __forceinline__ uint32_t block_reduce_256(uint32_t v, uint32_t* red) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint32_t t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(256) void k_tile_sums(const uint32_t* __restrict__ in, uint64_t n,
+                                                   uint32_t* __restrict__ tile_sums) {
+    __shared__ uint32_t red[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t i = base + k * 256 + threadIdx.x;
+        v += i < n ? in[i] : 0u;
+    }
+    const uint32_t t = block_reduce_256(v, red);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ in, uint64_t n,
+                                                    const uint32_t* __restrict__ tile_sums,
+                                                    uint32_t* __restrict__ out) {
+    __shared__ uint32_t red[4];
+    __shared__ uint32_t wsum[4];
+    // offset of this tile = sum of the tile sums before it
+    uint32_t pre = 0;
+    for (uint32_t t = threadIdx.x; t < blockIdx.x; t += 256) pre += tile_sums[t];
+    const uint32_t tile_off = block_reduce_256(pre, red);
+    // each thread owns 4 consecutive elements
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = base + k < n ? in[base + k] : 0u;
+        sum += v[k];
+    }
+    uint32_t x = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(x, d, 64);
@@ -481,13 +517,12 @@ __global__ __launch_bounds__(1024) void k_exclusive_scan(const uint32_t* __restr
     const uint32_t w = threadIdx.x >> 6;
     if (lane_id() == 63) wsum[w] = x;
     __syncthreads();
-    uint32_t run = 0;
+    uint32_t run = tile_off + x - sum;
     for (uint32_t k = 0; k < w; ++k) run += wsum[k];
-    run += x - sum;  // exclusive prefix of this thread's segment
-    for (uint64_t i = lo; i < hi; ++i) {
-        const uint32_t v = in[i];
-        out[i] = run;
-        run += v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
     }
 }
 
@@ -1352,16 +1387,24 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint32_t* d_hlist, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 4, (nblocks + 63) / 64));
+    // one lane per block: every header chain walks concurrently
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
     hipLaunchKernelGGL(k_count_records, dim3((uint32_t)grid), dim3(64), 0, st,
                        static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist);
     return hipGetLastError();
 }
 
-hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t st) {
-    hipLaunchKernelGGL(k_exclusive_scan, dim3(1), dim3(1024), 0, st, d_in, d_out, n);
+hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
+                              uint32_t* d_tile_scratch, hipStream_t st) {
+    const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_tile_sums, dim3((uint32_t)tiles), dim3(256), 0, st, d_in, n, d_tile_scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)tiles), dim3(256), 0, st, d_in, n, d_tile_scratch, d_out);
     return hipGetLastError();
 }
+
+uint64_t scan_scratch_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
 // One-time per device (per thread): the x^(8d) / init_xor(d) tables.
 static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {

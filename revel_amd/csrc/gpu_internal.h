@@ -34,8 +34,10 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 constexpr uint32_t kListPerBlock = 64;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint32_t* d_hlist, hipStream_t st);
+// d_tile_scratch: scan_scratch_words(n) u32 of device scratch.
 hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
-                              hipStream_t st);
+                              uint32_t* d_tile_scratch, hipStream_t st);
+uint64_t scan_scratch_words(uint64_t n);
 // variant 0 = production (uses the header list when given), 1 = round-1 kernel,
 // 2 = production kernel forced to walk headers itself.
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
@@ -69,4 +71,6 @@ struct revel_gpu_context {
     const void* hlist_image = nullptr;
     uint64_t hlist_nbytes = 0;
     const uint32_t* hlist_counts = nullptr;
+    uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
+    uint64_t scan_scratch_cap = 0;
 };

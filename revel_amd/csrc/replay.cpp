@@ -36,6 +36,7 @@ struct Window {
     uint32_t* d_counts = nullptr;  // RECORDS
     uint32_t* d_first = nullptr;
     uint32_t* d_hlist = nullptr;
+    uint32_t* d_scan = nullptr;
     revel_record_result* d_res = nullptr;
     uint32_t* d_masked = nullptr;  // FULL_BLOCKS
     uint8_t* d_ok = nullptr;
@@ -58,7 +59,7 @@ struct Ring {
             if (x.inflight) (void)hipEventSynchronize(x.e_done);
             if (x.h) (void)hipHostFree(x.h);
             if (x.h_sum) (void)hipHostFree(x.h_sum);
-            for (void* p : {x.d, (void*)x.d_counts, (void*)x.d_first, (void*)x.d_hlist, (void*)x.d_res,
+            for (void* p : {x.d, (void*)x.d_counts, (void*)x.d_first, (void*)x.d_hlist, (void*)x.d_scan, (void*)x.d_res,
                             (void*)x.d_masked, (void*)x.d_ok, (void*)x.d_sum})
                 if (p) (void)hipFree(p);
             for (hipEvent_t e : {x.e_h2d0, x.e_copied, x.e_k0, x.e_k1, x.e_done})
@@ -88,6 +89,7 @@ int ring_init(Ring& R, int nbuf) {
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_counts), nblocks * 4), "hipMalloc(counts)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_first), nblocks * 4), "hipMalloc(first)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), nblocks * revel::kListPerBlock * 4), "hipMalloc(hlist)");
+            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_scan), revel::scan_scratch_words(nblocks) * 4), "hipMalloc(scan)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_res), nblocks * kMaxRecordsPerBlock * sizeof(revel_record_result)),
                 "hipMalloc(records)");
         } else {
@@ -176,7 +178,7 @@ int replay(revel_gpu_context* ctx, uint64_t length, uint64_t base_offset, int mo
         const uint64_t nblocks = (x.len + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
         if (mode == REVEL_REPLAY_RECORDS) {
             TRY(revel::count_records(ctx->di, x.d, x.len, x.d_counts, x.d_hlist, comp), "count_records");
-            TRY(revel::exclusive_scan_u32(ctx->di, x.d_counts, x.d_first, nblocks, comp), "scan");
+            TRY(revel::exclusive_scan_u32(ctx->di, x.d_counts, x.d_first, nblocks, x.d_scan, comp), "scan");
             TRY(revel::verify_records(ctx->di, x.d, x.len, base_offset + off, x.d_first, x.d_res, x.d_hlist,
                                       x.d_counts, comp),
                 "verify_records");

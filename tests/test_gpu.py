@@ -314,3 +314,16 @@ def test_append_records_c1_and_readback(gpu_ctx):
     assert hashlib.sha256(host).digest() == z["sha256"].tobytes()
     res = gpu_ctx.verify_image(img, n)
     assert len(res) == 11250 and (res["status"] == 0).all()
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 1023, 1024, 1025, 4096, 131073, 1 << 20])
+def test_exclusive_scan(gpu_ctx, n):
+    from revel_amd._lib import check, lib
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 4682, n, dtype=np.uint32)
+    din = gpu_ctx.upload(a)
+    dout = gpu_ctx.alloc(4 * n)
+    check(lib().revel_gpu_exclusive_scan_u32(gpu_ctx.handle, din.ptr, dout.ptr, n, None))
+    gpu_ctx.sync()
+    want = np.concatenate([[0], np.cumsum(a, dtype=np.uint64)[:-1]]).astype(np.uint32)
+    assert np.array_equal(gpu_ctx.d2h(dout, 4 * n, np.uint32), want)
