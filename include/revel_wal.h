@@ -179,6 +179,33 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
                              uint64_t base_offset, const uint32_t* d_first,
                              revel_record_result* d_out, void* stream);
 
+/* ---- device replay reassembly (log_reader.rs:76-153 for a whole image) -- */
+/* One entry per event a Reader produces while reading the image from its
+ * start and continuing after every error: a logical record (FULL, or FIRST
+ * MIDDLE* LAST, all valid) with its payload gathered contiguously, or an error
+ * (the reader's Err(IOError)).  Incomplete fragments are dropped silently and
+ * a torn final record ends the image, as the reader does. */
+typedef struct revel_logical_record {
+    uint64_t file_offset;     /* header offset of the first physical record */
+    uint64_t payload_offset;  /* offset of the payload in the gathered buffer */
+    uint32_t length;          /* payload bytes (0 for an error event) */
+    uint32_t first_phys;      /* index range into the physical-record array */
+    uint32_t last_phys;
+    uint8_t status;           /* REVEL_LOGICAL_OK, or the REVEL_REC_* / BAD_TYPE error */
+    uint8_t reserved[3];
+} revel_logical_record;
+#define REVEL_LOGICAL_OK 0
+#define REVEL_LOGICAL_BAD_TYPE 4   /* record type outside FULL..LAST (log_reader.rs:126-128) */
+/* d_phys: the nphys results of revel_gpu_verify_records for d_image (whose
+ * byte 0 is file offset image_base, length image_len).  d_out needs nphys
+ * entries, d_payload image_len bytes.  checksum = 0 ignores CRC mismatches.
+ * Returns when done, with the event count in *nlogical and the gathered
+ * payload bytes in *payload_bytes. */
+int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image, uint64_t image_base, uint64_t image_len,
+                         const revel_record_result* d_phys, size_t nphys, int checksum,
+                         revel_logical_record* d_out, void* d_payload, uint64_t* nlogical,
+                         uint64_t* payload_bytes, void* stream);
+
 /* ---- device append framing (log_writer.rs:58-124 for a whole batch) ----- */
 /* Bytes that n successive add_record calls starting at block_offset would
  * append (headers, payloads, zero trailers). */

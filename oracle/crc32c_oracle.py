@@ -427,3 +427,37 @@ def synth_full_blocks(n: int, seed: int = 0x5EED0002, first: int = 0) -> np.ndar
     blocks[:, 0:4] = crcs.view(np.uint8).reshape(n, 4) if crcs.dtype.byteorder in "=<" else \
         crcs.astype("<u4").view(np.uint8).reshape(n, 4)
     return blocks
+
+
+# --- batch replay events (LogReader semantics, restated for device parity) ---
+EV_RECORD, EV_ERROR = 0, 1
+
+
+def replay_events(image: bytes, checksum: bool = True):
+    """The sequence a LogReader over ``image`` produces when every error is
+    caught and reading continues: ("record", first_file_offset, payload) or
+    ("error", file_offset, status).  Stops at EOF (incl. a torn tail).
+    initial_offset = 0 (log_reader.rs:76-153 / LogReader above)."""
+    rd = LogReader(image, checksum, 0)
+    out = []
+    while True:
+        start = rd.i
+        try:
+            rec = rd.read_record()
+        except CorruptionError as e:
+            r = e.args[0]
+            out.append(("error", r.file_offset, r.status))
+            continue
+        if rec is None:
+            return out
+        # first physical record of the returned logical record
+        j = rd.i - 1
+        phys = rd.records
+        if phys[j].rtype == FULL_TYPE:
+            first = phys[j].file_offset
+        else:
+            k = j
+            while phys[k].rtype != FIRST_TYPE:
+                k -= 1
+            first = phys[k].file_offset
+        out.append(("record", first, rec))

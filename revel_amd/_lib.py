@@ -44,6 +44,15 @@ class ReplayStats(Structure):
 
 REPLAY_RECORDS, REPLAY_FULL_BLOCKS = 0, 1
 
+
+class LogicalRecord(Structure):
+    _fields_ = [("file_offset", c_uint64), ("payload_offset", c_uint64), ("length", c_uint32),
+                ("first_phys", c_uint32), ("last_phys", c_uint32), ("status", c_uint8), ("reserved", c_uint8 * 3)]
+
+
+assert ctypes.sizeof(LogicalRecord) == 32
+LOGICAL_OK, LOGICAL_BAD_TYPE = 0, 4
+
 # name -> (restype, argtypes); every symbol declared in include/revel_wal.h
 SIGNATURES = {
     "revel_crc32c_value": (c_uint32, [c_void_p, c_size_t]),
@@ -95,6 +104,8 @@ SIGNATURES = {
     "revel_gpu_event_elapsed_ms": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_float)]),
     "revel_gpu_event_free": (c_int, [c_void_p, c_void_p]),
     "revel_last_error": (c_char_p, []),
+    "revel_gpu_reassemble": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_size_t, c_int, c_void_p,
+                                     c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_void_p]),
     "revel_log_framed_size": (c_uint64, [c_void_p, c_size_t, c_uint64]),
     "revel_gpu_append_records": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_uint64), c_void_p,
                                          c_size_t, POINTER(c_size_t), c_void_p]),

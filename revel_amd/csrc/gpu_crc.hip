@@ -467,57 +467,58 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
 // sums of the tiles before it and scans its own tile.
 constexpr uint32_t kScanTile = 1024;
 
-__device__ __forceinline__ uint32_t block_reduce_256(uint32_t v, uint32_t* red) {
+template <typename T>
+__device__ __forceinline__ T block_reduce_256(T v, T* red) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
     if (lane_id() == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    const uint32_t t = red[0] + red[1] + red[2] + red[3];
+    const T t = red[0] + red[1] + red[2] + red[3];
     __syncthreads();
     return t;
 }
 
-__global__ __launch_bounds__(256) void k_tile_sums(const uint32_t* __restrict__ in, uint64_t n,
-                                                   uint32_t* __restrict__ tile_sums) {
-    __shared__ uint32_t red[4];
+template <typename T>
+__global__ __launch_bounds__(256) void k_tile_sums(const T* __restrict__ in, uint64_t n, T* __restrict__ tile_sums) {
+    __shared__ T red[4];
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-    uint32_t v = 0;
+    T v = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint64_t i = base + k * 256 + threadIdx.x;
-        v += i < n ? in[i] : 0u;
+        v += i < n ? in[i] : T(0);
     }
-    const uint32_t t = block_reduce_256(v, red);
+    const T t = block_reduce_256<T>(v, red);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = t;
 }
 
-__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ in, uint64_t n,
-                                                    const uint32_t* __restrict__ tile_sums,
-                                                    uint32_t* __restrict__ out) {
-    __shared__ uint32_t red[4];
-    __shared__ uint32_t wsum[4];
+template <typename T>
+__global__ __launch_bounds__(256) void k_scan_apply(const T* __restrict__ in, uint64_t n, const T* __restrict__ tile_sums,
+                                                    T* __restrict__ out) {
+    __shared__ T red[4];
+    __shared__ T wsum[4];
     // offset of this tile = sum of the tile sums before it
-    uint32_t pre = 0;
+    T pre = 0;
     for (uint32_t t = threadIdx.x; t < blockIdx.x; t += 256) pre += tile_sums[t];
-    const uint32_t tile_off = block_reduce_256(pre, red);
+    const T tile_off = block_reduce_256<T>(pre, red);
     // each thread owns 4 consecutive elements
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
-    uint32_t v[4], sum = 0;
+    T v[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        v[k] = base + k < n ? in[base + k] : 0u;
+        v[k] = base + k < n ? in[base + k] : T(0);
         sum += v[k];
     }
-    uint32_t x = sum;
+    T x = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
+        const T y = __shfl_up(x, d, 64);
         if ((int)lane_id() >= d) x += y;
     }
     const uint32_t w = threadIdx.x >> 6;
     if (lane_id() == 63) wsum[w] = x;
     __syncthreads();
-    uint32_t run = tile_off + x - sum;
+    T run = tile_off + x - sum;
     for (uint32_t k = 0; k < w; ++k) run += wsum[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -943,6 +944,113 @@ __global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const 
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k)
                 if (i + k < d.len) pd[i + k] = src[i + k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Device replay reassembly (log_reader.rs:76-153, LevelDB-correct; the rules
+// of oracle LogReader / replay_events): physical records -> events in file
+// order: RECORD (FULL, or FIRST MIDDLE* LAST all valid) or ERROR (zero record,
+// length past the block that is not the torn tail of the image, checksum
+// mismatch when checking, unknown type).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool reasm_is_error(const revel_record_result& r, bool checksum, bool tail) {
+    if (r.status == REVEL_REC_ZERO) return true;
+    if (r.status == REVEL_REC_BAD_LENGTH) return !tail;
+    if (checksum && r.status == REVEL_REC_BAD_CHECKSUM) return true;
+    return r.type < REVEL_FULL_TYPE || r.type > REVEL_LAST_TYPE;
+}
+
+__global__ void k_reasm_classify(const revel_record_result* __restrict__ phys, uint64_t n, uint64_t image_end,
+                                 int checksum, uint32_t* __restrict__ ev_flag, uint64_t* __restrict__ ev_len,
+                                 uint32_t* __restrict__ ev_end) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const revel_record_result r = phys[i];
+        auto tail_of = [&](uint64_t k, const revel_record_result& q) {
+            return k == n - 1 && q.status == REVEL_REC_BAD_LENGTH && q.file_offset + kHeaderSize + q.length > image_end;
+        };
+        uint32_t flag = 0, end = (uint32_t)i;
+        uint64_t len = 0;
+        const bool tail = tail_of(i, r);
+        if (reasm_is_error(r, checksum, tail)) {
+            flag = 1;  // ERROR event
+        } else if (!tail) {
+            if (r.type == REVEL_FULL_TYPE) {
+                flag = 1;
+                len = r.length;
+            } else if (r.type == REVEL_FIRST_TYPE) {
+                uint64_t acc = r.length;
+                for (uint64_t j = i + 1; j < n; ++j) {
+                    const revel_record_result q = phys[j];
+                    if (reasm_is_error(q, checksum, tail_of(j, q)) || tail_of(j, q)) break;
+                    if (q.type == REVEL_MIDDLE_TYPE) {
+                        acc += q.length;
+                        continue;
+                    }
+                    if (q.type == REVEL_LAST_TYPE) {
+                        flag = 1;
+                        len = acc + q.length;
+                        end = (uint32_t)j;
+                    }
+                    break;  // FULL / FIRST: this fragment is dropped
+                }
+            }
+        }
+        ev_flag[i] = flag;
+        ev_len[i] = len;
+        ev_end[i] = end;
+    }
+}
+
+__global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint64_t n, uint64_t image_end, int checksum,
+                             const uint32_t* __restrict__ ev_flag, const uint32_t* __restrict__ ev_idx,
+                             const uint64_t* __restrict__ pay_off, const uint32_t* __restrict__ ev_end,
+                             revel_logical_record* __restrict__ out, uint64_t* __restrict__ frag_dst) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!ev_flag[i]) continue;
+        const revel_record_result r = phys[i];
+        const bool tail = i == n - 1 && r.status == REVEL_REC_BAD_LENGTH &&
+                          r.file_offset + kHeaderSize + r.length > image_end;
+        revel_logical_record o;
+        o.file_offset = r.file_offset;
+        o.payload_offset = pay_off[i];
+        o.first_phys = (uint32_t)i;
+        o.last_phys = ev_end[i];
+        o.reserved[0] = o.reserved[1] = o.reserved[2] = 0;
+        if (reasm_is_error(r, checksum, tail)) {
+            o.length = 0;
+            o.status = r.status == REVEL_REC_OK || (!checksum && r.status == REVEL_REC_BAD_CHECKSUM)
+                           ? REVEL_LOGICAL_BAD_TYPE
+                           : r.status;
+        } else {
+            uint64_t acc = 0;
+            for (uint64_t k = i; k <= ev_end[i]; ++k) {
+                frag_dst[k] = pay_off[i] + acc;
+                acc += phys[k].length;
+            }
+            o.length = (uint32_t)acc;
+            o.status = REVEL_LOGICAL_OK;
+        }
+        out[ev_idx[i]] = o;
+    }
+}
+
+// One wave per physical record that belongs to an emitted logical record.
+__global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image_base,
+                               const revel_record_result* __restrict__ phys, uint64_t n,
+                               const uint64_t* __restrict__ frag_dst, uint8_t* __restrict__ payload) {
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t k = blockIdx.x * (uint64_t)(blockDim.x / 64) + (threadIdx.x >> 6); k < n; k += waves) {
+        const uint64_t dst = frag_dst[k];
+        if (dst == ~0ull) continue;
+        const revel_record_result r = phys[k];
+        const uint8_t* src = image + (r.file_offset - image_base) + kHeaderSize;
+        uint8_t* d = payload + dst;
+        for (uint32_t i = lane_id() * 4; i < r.length; i += 256) {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b)
+                if (i + b < r.length) d[i + b] = src[i + b];
         }
     }
 }
@@ -1394,14 +1502,25 @@ hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nby
     return hipGetLastError();
 }
 
-hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
-                              uint32_t* d_tile_scratch, hipStream_t st) {
+template <typename T>
+static hipError_t exclusive_scan_t(const T* d_in, T* d_out, uint64_t n, T* d_tile_scratch, hipStream_t st) {
+    if (n == 0) return hipSuccess;
     const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_tile_sums, dim3((uint32_t)tiles), dim3(256), 0, st, d_in, n, d_tile_scratch);
+    hipLaunchKernelGGL(k_tile_sums<T>, dim3((uint32_t)tiles), dim3(256), 0, st, d_in, n, d_tile_scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)tiles), dim3(256), 0, st, d_in, n, d_tile_scratch, d_out);
+    hipLaunchKernelGGL(k_scan_apply<T>, dim3((uint32_t)tiles), dim3(256), 0, st, d_in, n, d_tile_scratch, d_out);
     return hipGetLastError();
+}
+
+hipError_t exclusive_scan_u32(const DeviceInfo&, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
+                              uint32_t* d_tile_scratch, hipStream_t st) {
+    return exclusive_scan_t<uint32_t>(d_in, d_out, n, d_tile_scratch, st);
+}
+
+hipError_t exclusive_scan_u64(const DeviceInfo&, const uint64_t* d_in, uint64_t* d_out, uint64_t n,
+                              uint64_t* d_tile_scratch, hipStream_t st) {
+    return exclusive_scan_t<uint64_t>(d_in, d_out, n, d_tile_scratch, st);
 }
 
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
@@ -1478,6 +1597,32 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     hipLaunchKernelGGL(k_verify_records2<true>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
                        static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr, lead, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
+                          int checksum, uint32_t* d_flag, uint64_t* d_len, uint32_t* d_end, hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));
+    hipLaunchKernelGGL(k_reasm_classify, dim3((uint32_t)grid), dim3(256), 0, st, d_phys, n, image_end, checksum, d_flag,
+                       d_len, d_end);
+    return hipGetLastError();
+}
+
+hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
+                      int checksum, const uint32_t* d_flag, const uint32_t* d_idx, const uint64_t* d_off,
+                      const uint32_t* d_end, revel_logical_record* d_out, uint64_t* d_frag_dst, hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));
+    hipLaunchKernelGGL(k_reasm_emit, dim3((uint32_t)grid), dim3(256), 0, st, d_phys, n, image_end, checksum, d_flag,
+                       d_idx, d_off, d_end, d_out, d_frag_dst);
+    return hipGetLastError();
+}
+
+hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
+                        const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
+                        hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 3) / 4));
+    hipLaunchKernelGGL(k_reasm_gather, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<const uint8_t*>(d_image),
+                       image_base, d_phys, n, d_frag_dst, static_cast<uint8_t*>(d_payload));
     return hipGetLastError();
 }
 

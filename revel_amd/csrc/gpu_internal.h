@@ -38,6 +38,16 @@ hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nby
 hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
                               uint32_t* d_tile_scratch, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
+hipError_t exclusive_scan_u64(const DeviceInfo& di, const uint64_t* d_in, uint64_t* d_out, uint64_t n,
+                              uint64_t* d_tile_scratch, hipStream_t st);
+hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
+                          int checksum, uint32_t* d_flag, uint64_t* d_len, uint32_t* d_end, hipStream_t st);
+hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
+                      int checksum, const uint32_t* d_flag, const uint32_t* d_idx, const uint64_t* d_off,
+                      const uint32_t* d_end, revel_logical_record* d_out, uint64_t* d_frag_dst, hipStream_t st);
+hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
+                        const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
+                        hipStream_t st);
 // variant 0 = production (uses the header list when given), 1 = round-1 kernel,
 // 2 = production kernel forced to walk headers itself.
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,

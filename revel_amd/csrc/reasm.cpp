@@ -1,0 +1,77 @@
+// reasm.cpp -- revel_gpu_reassemble: the C-ABI driver of the device replay
+// reassembly kernels (classify -> two scans -> emit -> gather).  The rules
+// are log_reader.rs:76-153 made LevelDB-correct.
+#include <hip/hip_runtime_api.h>
+#include <string.h>
+
+#include <vector>
+
+#include "gpu_internal.h"
+#include "revel_wal.h"
+
+using revel::set_error;
+
+namespace {
+
+struct Scratch {
+    std::vector<void*> ptrs;
+    ~Scratch() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    hipError_t get(T** p, uint64_t n) {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, (n ? n : 1) * sizeof(T));
+        if (e == hipSuccess) ptrs.push_back(q);
+        *p = static_cast<T*>(q);
+        return e;
+    }
+};
+
+}  // namespace
+
+extern "C" int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image, uint64_t image_base,
+                                    uint64_t image_len, const revel_record_result* d_phys, size_t nphys, int checksum,
+                                    revel_logical_record* d_out, void* d_payload, uint64_t* nlogical,
+                                    uint64_t* payload_bytes, void* stream) {
+    if (!ctx || !nlogical || !payload_bytes) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
+    *nlogical = 0;
+    *payload_bytes = 0;
+    if (nphys == 0) return REVEL_OK;
+    if (!d_image || !d_phys || !d_out || !d_payload) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const uint64_t n = nphys;
+    const uint64_t tiles = revel::scan_scratch_words(n);
+    Scratch S;
+    uint32_t *flag, *end, *idx, *t32;
+    uint64_t *len, *off, *dst, *t64;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = S.get(&flag, n);
+    if (e == hipSuccess) e = S.get(&end, n);
+    if (e == hipSuccess) e = S.get(&idx, n);
+    if (e == hipSuccess) e = S.get(&t32, tiles);
+    if (e == hipSuccess) e = S.get(&len, n);
+    if (e == hipSuccess) e = S.get(&off, n);
+    if (e == hipSuccess) e = S.get(&dst, n);
+    if (e == hipSuccess) e = S.get(&t64, tiles);
+    const uint64_t image_end = image_base + image_len;
+    if (e == hipSuccess) e = revel::reasm_classify(ctx->di, d_phys, n, image_end, checksum, flag, len, end, st);
+    if (e == hipSuccess) e = revel::exclusive_scan_u32(ctx->di, flag, idx, n, t32, st);
+    if (e == hipSuccess) e = revel::exclusive_scan_u64(ctx->di, len, off, n, t64, st);
+    if (e == hipSuccess) e = hipMemsetAsync(dst, 0xFF, n * sizeof(uint64_t), st);
+    if (e == hipSuccess)
+        e = revel::reasm_emit(ctx->di, d_phys, n, image_end, checksum, flag, idx, off, end, d_out, dst, st);
+    if (e == hipSuccess) e = revel::reasm_gather(ctx->di, d_image, image_base, d_phys, n, dst, d_payload, st);
+    uint32_t last_idx = 0, last_flag = 0;
+    uint64_t last_off = 0, last_len = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&last_idx, idx + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&last_flag, flag + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&last_off, off + n - 1, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&last_len, len + n - 1, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return set_error(REVEL_IO_ERROR, "reassemble: %s", hipGetErrorString(e));
+    *nlogical = (uint64_t)last_idx + last_flag;
+    *payload_bytes = last_off + last_len;
+    return REVEL_OK;
+}

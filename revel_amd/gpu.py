@@ -15,6 +15,8 @@ import numpy as np
 from ._lib import (BLOCK_SIZE, REPLAY_FULL_BLOCKS, REPLAY_RECORDS, RecordResult, ReplayStats, check,
                    lib)
 
+LOGICAL_DTYPE = np.dtype([("file_offset", "<u8"), ("payload_offset", "<u8"), ("length", "<u4"),
+                          ("first_phys", "<u4"), ("last_phys", "<u4"), ("status", "u1"), ("reserved", "u1", (3,))])
 RECORD_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("stored_crc", "<u4"),
                          ("computed_crc", "<u4"), ("type", "u1"), ("status", "u1"), ("reserved", "u1", (2,))])
 assert RECORD_DTYPE.itemsize == ctypes.sizeof(RecordResult)
@@ -215,3 +217,21 @@ class GpuContext:
         check(L.revel_gpu_append_records(self._h, payloads.ptr, lens.ctypes.data, len(lens), ctypes.byref(bo),
                                          img.ptr, img.nbytes, ctypes.byref(n), None))
         return img, n.value, bo.value
+
+    # ---- device replay reassembly ----
+    def reassemble(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0, checksum: bool = True):
+        """Verify + reassemble a device-resident WAL image on the GPU.  Returns
+        (events: LOGICAL_DTYPE array, payload bytes: np.uint8 array, phys)."""
+        phys = self.verify_image(image, nbytes, base_offset)
+        n = len(phys)
+        if n == 0:
+            return np.zeros(0, LOGICAL_DTYPE), np.zeros(0, np.uint8), phys
+        dphys = self.upload(phys.view(np.uint8))
+        out = self.alloc(n * LOGICAL_DTYPE.itemsize)
+        pay = self.alloc(max(1, nbytes))
+        nl, pb = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().revel_gpu_reassemble(self._h, image.ptr, base_offset, nbytes, dphys.ptr, n, 1 if checksum else 0,
+                                         out.ptr, pay.ptr, ctypes.byref(nl), ctypes.byref(pb), None))
+        ev = self.d2h(out, nl.value * LOGICAL_DTYPE.itemsize).view(LOGICAL_DTYPE)
+        payload = self.d2h(pay, pb.value) if pb.value else np.zeros(0, np.uint8)
+        return ev, payload, phys

@@ -327,3 +327,40 @@ def test_exclusive_scan(gpu_ctx, n):
     gpu_ctx.sync()
     want = np.concatenate([[0], np.cumsum(a, dtype=np.uint64)[:-1]]).astype(np.uint32)
     assert np.array_equal(gpu_ctx.d2h(dout, 4 * n, np.uint32), want)
+
+
+# ---- device replay reassembly vs the oracle reader's event sequence ----
+def check_reassembly(gpu_ctx, img, checksum=True):
+    d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    ev, payload, _ = gpu_ctx.reassemble(d, len(img), checksum=checksum)
+    want = po.replay_events(img, checksum=checksum)
+    assert len(ev) == len(want)
+    for e, w in zip(ev, want):
+        assert int(e["file_offset"]) == w[1]
+        if w[0] == "record":
+            assert e["status"] == 0
+            p0 = int(e["payload_offset"])
+            assert payload[p0:p0 + int(e["length"])].tobytes() == w[2]
+        else:
+            assert e["status"] != 0 and e["length"] == 0
+
+
+@pytest.mark.parametrize("checksum", [True, False])
+def test_reassemble_golden(gpu_ctx, golden_index, checksum):
+    for name in golden_index:
+        check_reassembly(gpu_ctx, golden_image(name), checksum)
+
+
+def test_reassemble_mixed_corruption(gpu_ctx):
+    rng = np.random.default_rng(31)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 120000, 80)]
+    img = bytearray(oc.write_image(recs))
+    ref = oc.walk(bytes(img))
+    for v in rng.choice(len(ref), 12, replace=False):       # flip payload / type bytes
+        off = int(ref["file_offset"][v])
+        if v % 3 == 0:
+            img[off + 6] = 9                                  # unknown type
+        elif ref["length"][v] > 0:
+            img[off + 7 + int(rng.integers(0, int(ref["length"][v])))] ^= 0x40
+    check_reassembly(gpu_ctx, bytes(img), True)
+    check_reassembly(gpu_ctx, bytes(img), False)
