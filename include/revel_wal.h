@@ -206,6 +206,50 @@ int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image, uint64_t i
                          revel_logical_record* d_out, void* d_payload, uint64_t* nlogical,
                          uint64_t* payload_bytes, void* stream);
 
+/* ---- device WriteBatch decode (write_batch.rs:79-128 + insert_into :178-181)
+ * Each reassembled logical record of a WAL is one WriteBatch rep:
+ * [seq fixed64][count fixed32] then count x (tag, varint32 klen, key
+ * [, varint32 vlen, value]).  Decoding is LevelDB-correct (the reference's
+ * iterate() never advances past a deletion and sequence() reads offset 8; see
+ * DESIGN.md section 4.8).  Entry i of a batch carries sequence seq + i
+ * (MemTableInserter, write_batch.rs:148-158). */
+#define REVEL_BATCH_HEADER 12
+#define REVEL_TYPE_DELETION 0   /* dbformat.rs:24-28 ValueType */
+#define REVEL_TYPE_VALUE 1
+#define REVEL_BATCH_OK 0
+#define REVEL_BATCH_TOO_SMALL 1    /* < 12 bytes */
+#define REVEL_BATCH_BAD_ENTRY 2    /* key/value varint or length out of range */
+#define REVEL_BATCH_BAD_TAG 3      /* tag not 0/1 (dbformat.rs:36 panics) */
+#define REVEL_BATCH_WRONG_COUNT 4  /* decoded entries != header count */
+#define REVEL_BATCH_NOT_RECORD 5   /* the logical event was a log error */
+typedef struct revel_batch_info {
+    uint64_t sequence;     /* header sequence (rep[0..8]) */
+    uint64_t first_entry;  /* index of its first entry in the entry table */
+    uint32_t count;        /* header count (rep[8..12]) */
+    uint32_t nentries;     /* entries decoded (those before an error, on error) */
+    uint8_t status;        /* REVEL_BATCH_* */
+    uint8_t reserved[7];
+} revel_batch_info;
+typedef struct revel_batch_entry {
+    uint64_t sequence;      /* batch sequence + entry index */
+    uint64_t key_offset;    /* offsets into the gathered payload buffer */
+    uint64_t value_offset;  /* (value_len 0 and offset past the key for a deletion) */
+    uint32_t key_len;
+    uint32_t value_len;
+    uint32_t batch;         /* logical record index */
+    uint8_t type;           /* REVEL_TYPE_VALUE / REVEL_TYPE_DELETION */
+    uint8_t reserved[3];
+} revel_batch_entry;
+/* d_payload / d_logical: the outputs of revel_gpu_reassemble (nlogical
+ * events over payload_bytes bytes).  d_info receives nlogical infos; entries
+ * go to d_entries (capacity entries_cap; payload_bytes / 2 always suffices,
+ * every entry being at least 2 bytes).  *nentries receives the total entry
+ * count; REVEL_INVALID_ARGUMENT if it exceeds entries_cap (infos are still
+ * written, entries past the cap are not).  Returns when done. */
+int revel_gpu_decode_batches(revel_gpu_context* ctx, const void* d_payload, uint64_t payload_bytes,
+                             const revel_logical_record* d_logical, size_t nlogical, revel_batch_info* d_info,
+                             revel_batch_entry* d_entries, size_t entries_cap, uint64_t* nentries, void* stream);
+
 /* ---- device append framing (log_writer.rs:58-124 for a whole batch) ----- */
 /* Bytes that n successive add_record calls starting at block_offset would
  * append (headers, payloads, zero trailers). */

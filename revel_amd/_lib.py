@@ -52,6 +52,9 @@ class LogicalRecord(Structure):
 
 assert ctypes.sizeof(LogicalRecord) == 32
 LOGICAL_OK, LOGICAL_BAD_TYPE = 0, 4
+BATCH_HEADER = 12
+TYPE_DELETION, TYPE_VALUE = 0, 1
+BATCH_OK, BATCH_TOO_SMALL, BATCH_BAD_ENTRY, BATCH_BAD_TAG, BATCH_WRONG_COUNT, BATCH_NOT_RECORD = 0, 1, 2, 3, 4, 5
 
 # name -> (restype, argtypes); every symbol declared in include/revel_wal.h
 SIGNATURES = {
@@ -106,6 +109,8 @@ SIGNATURES = {
     "revel_last_error": (c_char_p, []),
     "revel_gpu_reassemble": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_size_t, c_int, c_void_p,
                                      c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_void_p]),
+    "revel_gpu_decode_batches": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_size_t, c_void_p, c_void_p,
+                                         c_size_t, POINTER(c_uint64), c_void_p]),
     "revel_log_framed_size": (c_uint64, [c_void_p, c_size_t, c_uint64]),
     "revel_gpu_append_records": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_uint64), c_void_p,
                                          c_size_t, POINTER(c_size_t), c_void_p]),

@@ -65,6 +65,31 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
                          void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st);
 
+hipError_t batch_count(const DeviceInfo& di, const void* d_payload, uint64_t payload_bytes,
+                       const revel_logical_record* d_logical, uint64_t n, revel_batch_info* d_info, uint64_t* d_nent,
+                       hipStream_t st);
+hipError_t batch_emit(const DeviceInfo& di, const void* d_payload, uint64_t payload_bytes,
+                      const revel_logical_record* d_logical, uint64_t n, const uint64_t* d_first,
+                      revel_batch_info* d_info, revel_batch_entry* d_entries, uint64_t cap, hipStream_t st);
+
+// Device scratch freed when the call that allocated it returns.
+struct DeviceScratch {
+    void* ptrs[16] = {};
+    int n = 0;
+    ~DeviceScratch() {
+        for (int i = 0; i < n; ++i) (void)hipFree(ptrs[i]);
+    }
+    template <typename T>
+    hipError_t get(T** p, uint64_t count) {
+        void* q = nullptr;
+        if (n == 16) return hipErrorOutOfMemory;
+        hipError_t e = hipMalloc(&q, (count ? count : 1) * sizeof(T));
+        if (e == hipSuccess) ptrs[n++] = q;
+        *p = static_cast<T*>(q);
+        return e;
+    }
+};
+
 // Set the thread-local error string; returns code.
 int set_error(int code, const char* fmt, ...);
 

@@ -4,31 +4,10 @@
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 
-#include <vector>
-
 #include "gpu_internal.h"
 #include "revel_wal.h"
 
 using revel::set_error;
-
-namespace {
-
-struct Scratch {
-    std::vector<void*> ptrs;
-    ~Scratch() {
-        for (void* p : ptrs) (void)hipFree(p);
-    }
-    template <typename T>
-    hipError_t get(T** p, uint64_t n) {
-        void* q = nullptr;
-        hipError_t e = hipMalloc(&q, (n ? n : 1) * sizeof(T));
-        if (e == hipSuccess) ptrs.push_back(q);
-        *p = static_cast<T*>(q);
-        return e;
-    }
-};
-
-}  // namespace
 
 extern "C" int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image, uint64_t image_base,
                                     uint64_t image_len, const revel_record_result* d_phys, size_t nphys, int checksum,
@@ -43,7 +22,7 @@ extern "C" int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image,
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const uint64_t n = nphys;
     const uint64_t tiles = revel::scan_scratch_words(n);
-    Scratch S;
+    revel::DeviceScratch S;
     uint32_t *flag, *end, *idx, *t32;
     uint64_t *len, *off, *dst, *t64;
     hipError_t e = hipSuccess;

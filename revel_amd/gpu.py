@@ -17,6 +17,12 @@ from ._lib import (BLOCK_SIZE, REPLAY_FULL_BLOCKS, REPLAY_RECORDS, RecordResult,
 
 LOGICAL_DTYPE = np.dtype([("file_offset", "<u8"), ("payload_offset", "<u8"), ("length", "<u4"),
                           ("first_phys", "<u4"), ("last_phys", "<u4"), ("status", "u1"), ("reserved", "u1", (3,))])
+BATCH_INFO_DTYPE = np.dtype([("sequence", "<u8"), ("first_entry", "<u8"), ("count", "<u4"), ("nentries", "<u4"),
+                             ("status", "u1"), ("reserved", "u1", (7,))])
+BATCH_ENTRY_DTYPE = np.dtype([("sequence", "<u8"), ("key_offset", "<u8"), ("value_offset", "<u8"),
+                              ("key_len", "<u4"), ("value_len", "<u4"), ("batch", "<u4"), ("type", "u1"),
+                              ("reserved", "u1", (3,))])
+assert BATCH_INFO_DTYPE.itemsize == 32 and BATCH_ENTRY_DTYPE.itemsize == 40
 RECORD_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("stored_crc", "<u4"),
                          ("computed_crc", "<u4"), ("type", "u1"), ("status", "u1"), ("reserved", "u1", (2,))])
 assert RECORD_DTYPE.itemsize == ctypes.sizeof(RecordResult)
@@ -219,19 +225,54 @@ class GpuContext:
         return img, n.value, bo.value
 
     # ---- device replay reassembly ----
-    def reassemble(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0, checksum: bool = True):
-        """Verify + reassemble a device-resident WAL image on the GPU.  Returns
-        (events: LOGICAL_DTYPE array, payload bytes: np.uint8 array, phys)."""
+    def reassemble_device(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0, checksum: bool = True):
+        """Verify + reassemble a device-resident WAL image, leaving the results
+        in HBM: (events DeviceBuffer, nlogical, payload DeviceBuffer,
+        payload_bytes, phys host array)."""
         phys = self.verify_image(image, nbytes, base_offset)
         n = len(phys)
-        if n == 0:
-            return np.zeros(0, LOGICAL_DTYPE), np.zeros(0, np.uint8), phys
-        dphys = self.upload(phys.view(np.uint8))
-        out = self.alloc(n * LOGICAL_DTYPE.itemsize)
+        out = self.alloc(max(1, n) * LOGICAL_DTYPE.itemsize)
         pay = self.alloc(max(1, nbytes))
+        if n == 0:
+            return out, 0, pay, 0, phys
+        dphys = self.upload(phys.view(np.uint8))
         nl, pb = ctypes.c_uint64(), ctypes.c_uint64()
         check(lib().revel_gpu_reassemble(self._h, image.ptr, base_offset, nbytes, dphys.ptr, n, 1 if checksum else 0,
                                          out.ptr, pay.ptr, ctypes.byref(nl), ctypes.byref(pb), None))
-        ev = self.d2h(out, nl.value * LOGICAL_DTYPE.itemsize).view(LOGICAL_DTYPE)
-        payload = self.d2h(pay, pb.value) if pb.value else np.zeros(0, np.uint8)
+        return out, nl.value, pay, pb.value, phys
+
+    def reassemble(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0, checksum: bool = True):
+        """Verify + reassemble a device-resident WAL image on the GPU.  Returns
+        (events: LOGICAL_DTYPE array, payload bytes: np.uint8 array, phys)."""
+        out, nl, pay, pb, phys = self.reassemble_device(image, nbytes, base_offset, checksum)
+        ev = self.d2h(out, nl * LOGICAL_DTYPE.itemsize).view(LOGICAL_DTYPE) if nl else np.zeros(0, LOGICAL_DTYPE)
+        payload = self.d2h(pay, pb) if pb else np.zeros(0, np.uint8)
         return ev, payload, phys
+
+    # ---- device WriteBatch decode ----
+    def decode_batches_device(self, payload: DeviceBuffer, payload_bytes: int, events: DeviceBuffer, nlogical: int,
+                              entries_cap: Optional[int] = None):
+        """Decode every logical record as a WriteBatch on the GPU:
+        (info DeviceBuffer, entries DeviceBuffer, nentries)."""
+        cap = payload_bytes // 2 if entries_cap is None else entries_cap
+        info = self.alloc(max(1, nlogical) * BATCH_INFO_DTYPE.itemsize)
+        ent = self.alloc(max(1, cap) * BATCH_ENTRY_DTYPE.itemsize)
+        ne = ctypes.c_uint64()
+        check(lib().revel_gpu_decode_batches(self._h, payload.ptr, payload_bytes, events.ptr, nlogical, info.ptr,
+                                             ent.ptr, cap, ctypes.byref(ne), None))
+        return info, ent, ne.value
+
+    def replay_batches(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0, checksum: bool = True):
+        """WAL image in HBM -> verified, reassembled, decoded WriteBatches.
+        Returns (events, payload, infos BATCH_INFO_DTYPE, entries
+        BATCH_ENTRY_DTYPE) as host arrays."""
+        out, nl, pay, pb, _ = self.reassemble_device(image, nbytes, base_offset, checksum)
+        ev = self.d2h(out, nl * LOGICAL_DTYPE.itemsize).view(LOGICAL_DTYPE) if nl else np.zeros(0, LOGICAL_DTYPE)
+        payload = self.d2h(pay, pb) if pb else np.zeros(0, np.uint8)
+        if nl == 0:
+            return ev, payload, np.zeros(0, BATCH_INFO_DTYPE), np.zeros(0, BATCH_ENTRY_DTYPE)
+        info, ent, ne = self.decode_batches_device(pay, pb, out, nl)
+        infos = self.d2h(info, nl * BATCH_INFO_DTYPE.itemsize).view(BATCH_INFO_DTYPE)
+        ents = self.d2h(ent, ne * BATCH_ENTRY_DTYPE.itemsize).view(BATCH_ENTRY_DTYPE) if ne else \
+            np.zeros(0, BATCH_ENTRY_DTYPE)
+        return ev, payload, infos, ents

@@ -124,3 +124,60 @@ def test_reader_semantics_edges(golden_index):
     with pytest.raises(po.CorruptionError):
         po.read_all(golden_image("zero_block"))
     assert len(po.read_all(golden_image("corrupt_bit"), checksum=False)) == 20
+
+
+# ---- WriteBatch / varint restatement (write_batch.rs, coding.rs) ----
+from oracle import write_batch_oracle as wb  # noqa: E402
+
+
+def test_varint32_roundtrip():  # coding.rs:173-191
+    s = b"".join(wb.put_varint32(((i // 32) << (i % 32)) & 0xFFFFFFFF) for i in range(32 * 32))
+    off = 0
+    for i in range(32 * 32):
+        v, used = wb.get_varint32(s, off, len(s))
+        assert v == ((i // 32) << (i % 32)) & 0xFFFFFFFF
+        assert used == len(wb.put_varint32(v))
+        off += used
+    assert off == len(s)
+
+
+def test_varint32_overflow_and_truncation():  # coding.rs:193-212
+    assert wb.get_varint32(bytes([129, 130, 131, 132, 133, 17]), 0, 6) is None
+    big = wb.put_varint32((1 << 31) + 100)
+    for n in range(len(big)):
+        assert wb.get_varint32(big, 0, n) is None
+    assert wb.get_varint32(big, 0, len(big)) == ((1 << 31) + 100, 5)
+
+
+def test_write_batch_encode_decode():
+    b = wb.WriteBatch()
+    assert b.contents() == bytes(12) and b.count() == 0
+    b.put(b"foo", b"bar")
+    b.delete(b"box")
+    b.put(b"baz", b"boo")
+    b.set_sequence(100)
+    rep = b.contents()
+    assert rep[:12] == (100).to_bytes(8, "little") + (3).to_bytes(4, "little")
+    assert rep[12:] == b"\x01\x03foo\x03bar\x00\x03box\x01\x03baz\x03boo"
+    st, seq, cnt, ents = wb.decode(rep)
+    assert (st, seq, cnt) == (wb.OK, 100, 3)
+    assert ents == [(100, 1, b"foo", b"bar"), (101, 0, b"box", b""), (102, 1, b"baz", b"boo")]
+
+
+def test_write_batch_malformed():
+    from tests_gen import malformed_batches
+    for name, rep, want in malformed_batches():
+        assert wb.decode(rep)[0] == want, name
+    # entries before an error are still reported (LevelDB hands them over)
+    st, _, _, ents = wb.decode(dict((n, r) for n, r, _ in malformed_batches())["bad_tag"])
+    assert st == wb.BAD_TAG and [e[2] for e in ents] == [b"k", b"gone"]
+
+
+def test_batch_log_sequences_follow_db_write():  # db.rs:95-112
+    from tests_gen import batch_log
+    reps = batch_log(np.random.default_rng(1), 30, first_sequence=5)
+    nxt = 5
+    for r in reps:
+        st, seq, cnt, ents = wb.decode(r)
+        assert st == wb.OK and seq == nxt and len(ents) == cnt
+        nxt += cnt
