@@ -299,9 +299,18 @@ const char* revel_last_error(void);
  * mode REVEL_REPLAY_RECORDS verifies every physical record (config C3/C5
  * layout); REVEL_REPLAY_FULL_BLOCKS treats every block as one FULL record
  * (config C2 layout).  Windows are whole blocks; records never cross a block,
- * so window boundaries are exact. */
+ * so window boundaries are exact.
+ * For revel_gpu_replay_file, one REVEL_REPLAY_IO_* flag may be or-ed into mode
+ * to choose how windows are read (SequentialFile::read, env.rs:162-169, in
+ * bulk): a read-only MAP_SHARED mapping copied by the io threads (default;
+ * the file must not shrink during the replay), buffered pread, or O_DIRECT
+ * pread (REVEL_NOT_SUPPORT where the file system refuses O_DIRECT; there is
+ * no silent fallback).  DESIGN.md section 4.4 has the measured rates. */
 #define REVEL_REPLAY_RECORDS 0
 #define REVEL_REPLAY_FULL_BLOCKS 1
+#define REVEL_REPLAY_IO_MMAP 0x00
+#define REVEL_REPLAY_IO_PREAD 0x10
+#define REVEL_REPLAY_IO_DIRECT 0x20
 typedef struct revel_replay_stats {
     uint64_t bytes;            /* bytes replayed */
     uint64_t windows;          /* windows processed */

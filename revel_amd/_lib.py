@@ -43,6 +43,7 @@ class ReplayStats(Structure):
 
 
 REPLAY_RECORDS, REPLAY_FULL_BLOCKS = 0, 1
+REPLAY_IO = {"mmap": 0x00, "pread": 0x10, "direct": 0x20}
 
 
 class LogicalRecord(Structure):

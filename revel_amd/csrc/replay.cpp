@@ -14,6 +14,7 @@
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -106,7 +107,9 @@ int ring_init(Ring& R, int nbuf) {
 template <typename F>
 double parallel_fill(int threads, uint64_t len, F&& part) {
     auto t0 = std::chrono::steady_clock::now();
-    const uint64_t chunk = std::max<uint64_t>(1 << 20, (len + threads - 1) / threads);
+    // 64 KiB-aligned pieces (O_DIRECT needs page-aligned offsets and sizes)
+    const uint64_t per = (len + threads - 1) / threads;
+    const uint64_t chunk = std::max<uint64_t>(1 << 20, (per + 65535) / 65536 * 65536);
     std::vector<std::thread> pool;
     for (uint64_t off = 0; off < len; off += chunk) {
         const uint64_t n = std::min(chunk, len - off);
@@ -139,6 +142,7 @@ template <typename Fill>
 int replay(revel_gpu_context* ctx, uint64_t length, uint64_t base_offset, int mode, size_t window_bytes, int nbuffers,
            int io_threads, revel_replay_stats* out, Fill&& fill) {
     if (!ctx || !out) return set_error(REVEL_INVALID_ARGUMENT, "null ctx/out");
+    mode &= 0x0F;  // the IO flags were consumed by the caller
     if (mode != REVEL_REPLAY_RECORDS && mode != REVEL_REPLAY_FULL_BLOCKS)
         return set_error(REVEL_INVALID_ARGUMENT, "bad replay mode %d", mode);
     if (base_offset % REVEL_BLOCK_SIZE)
@@ -212,18 +216,46 @@ extern "C" {
 int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t offset, uint64_t length, int mode,
                           size_t window_bytes, int nbuffers, int io_threads, revel_replay_stats* out) {
     if (!path) return set_error(REVEL_INVALID_ARGUMENT, "null path");
-    int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    const int io = mode & 0xF0;
+    if (io != REVEL_REPLAY_IO_PREAD && io != REVEL_REPLAY_IO_MMAP && io != REVEL_REPLAY_IO_DIRECT)
+        return set_error(REVEL_INVALID_ARGUMENT, "bad replay io flag 0x%x", io);
+    int fd = ::open(path, O_RDONLY | O_CLOEXEC | (io == REVEL_REPLAY_IO_DIRECT ? O_DIRECT : 0));
+    if (fd < 0 && io == REVEL_REPLAY_IO_DIRECT && errno == EINVAL)
+        return set_error(REVEL_NOT_SUPPORT, "open(%s, O_DIRECT): not supported by this file system", path);
     if (fd < 0) return set_error(REVEL_NOT_FOUND, "open(%s): %s", path, strerror(errno));
-    if (length == 0) {
-        off_t end = ::lseek(fd, 0, SEEK_END);
-        length = end > (off_t)offset ? (uint64_t)end - offset : 0;
+    const off_t end = ::lseek(fd, 0, SEEK_END);
+    if (length == 0) length = end > (off_t)offset ? (uint64_t)end - offset : 0;
+    if (end < 0 || offset + length > (uint64_t)end) {
+        ::close(fd);
+        return set_error(REVEL_INVALID_ARGUMENT, "range [%llu, +%llu) past the end of %s", (unsigned long long)offset,
+                         (unsigned long long)length, path);
     }
     bool io_error = false;
-    int rc = replay(ctx, length, offset, mode, window_bytes, nbuffers, io_threads, out,
+    int rc;
+    if (io == REVEL_REPLAY_IO_MMAP) {
+        // offset is block- (hence page-) aligned; the io threads copy straight
+        // from the page cache into the pinned window (no read(2) per piece)
+        void* m = length ? ::mmap(nullptr, length, PROT_READ, MAP_SHARED, fd, (off_t)offset) : nullptr;
+        if (m == MAP_FAILED) {
+            ::close(fd);
+            return set_error(REVEL_IO_ERROR, "mmap(%s): %s", path, strerror(errno));
+        }
+        if (m) (void)::madvise(m, length, MADV_SEQUENTIAL);
+        const uint8_t* src = static_cast<const uint8_t*>(m);
+        rc = replay(ctx, length, offset, mode, window_bytes, nbuffers, io_threads, out,
+                    [&](uint8_t* dst, uint64_t rel, uint64_t n) { memcpy(dst, src + rel, n); });
+        if (m) ::munmap(m, length);
+    } else {
+        const uint64_t align = io == REVEL_REPLAY_IO_DIRECT ? 4096 : 1;
+        rc = replay(ctx, length, offset, mode, window_bytes, nbuffers, io_threads, out,
                     [&](uint8_t* dst, uint64_t rel, uint64_t n) {
+                        // O_DIRECT: pieces start page-aligned; the request is
+                        // rounded up (the window has room: its size is whole
+                        // blocks) and the kernel stops at end of file
+                        const uint64_t want = (n + align - 1) / align * align;
                         uint64_t done = 0;
                         while (done < n) {
-                            ssize_t r = ::pread(fd, dst + done, n - done, (off_t)(offset + rel + done));
+                            ssize_t r = ::pread(fd, dst + done, want - done, (off_t)(offset + rel + done));
                             if (r < 0 && errno == EINTR) continue;
                             if (r <= 0) {
                                 memset(dst + done, 0, n - done);
@@ -233,6 +265,7 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
                             done += (uint64_t)r;
                         }
                     });
+    }
     ::close(fd);
     if (rc == REVEL_OK && io_error) return set_error(REVEL_IO_ERROR, "short read from %s", path);
     return rc;
@@ -241,6 +274,7 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
 int revel_gpu_replay_memory(revel_gpu_context* ctx, const uint8_t* image, uint64_t length, uint64_t base_offset,
                             int mode, size_t window_bytes, int nbuffers, int io_threads, revel_replay_stats* out) {
     if (!image && length) return set_error(REVEL_INVALID_ARGUMENT, "null image");
+    if (mode & 0xF0) return set_error(REVEL_INVALID_ARGUMENT, "io flags apply to revel_gpu_replay_file only");
     return replay(ctx, length, base_offset, mode, window_bytes, nbuffers, io_threads, out,
                   [&](uint8_t* dst, uint64_t rel, uint64_t n) { memcpy(dst, image + rel, n); });
 }

@@ -12,7 +12,7 @@ from typing import Optional, Tuple
 
 import numpy as np
 
-from ._lib import (BLOCK_SIZE, REPLAY_FULL_BLOCKS, REPLAY_RECORDS, RecordResult, ReplayStats, check,
+from ._lib import (BLOCK_SIZE, REPLAY_FULL_BLOCKS, REPLAY_IO, REPLAY_RECORDS, RecordResult, ReplayStats, check,
                    lib)
 
 LOGICAL_DTYPE = np.dtype([("file_offset", "<u8"), ("payload_offset", "<u8"), ("length", "<u4"),
@@ -203,10 +203,12 @@ class GpuContext:
         return st.as_dict()
 
     def replay_file(self, path: str, offset: int = 0, length: int = 0, full_blocks: bool = False,
-                    window_bytes: int = 64 << 20, nbuffers: int = 4, io_threads: int = 8) -> dict:
+                    window_bytes: int = 64 << 20, nbuffers: int = 4, io_threads: int = 8, io: str = "mmap") -> dict:
+        """io: "mmap" (page cache copied by the io threads; default), "pread"
+        (buffered) or "direct" (O_DIRECT; RevelError NOT_SUPPORT where refused)."""
         st = ReplayStats()
         check(lib().revel_gpu_replay_file(self._h, path.encode(), offset, length,
-                                          REPLAY_FULL_BLOCKS if full_blocks else REPLAY_RECORDS,
+                                          (REPLAY_FULL_BLOCKS if full_blocks else REPLAY_RECORDS) | REPLAY_IO[io],
                                           window_bytes, nbuffers, io_threads, ctypes.byref(st)))
         return st.as_dict()
 

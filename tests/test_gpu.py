@@ -284,6 +284,36 @@ def test_replay_full_blocks_and_file(gpu_ctx, tmp_path):
     assert (st["units"], st["bad"], st["first_bad_offset"]) == (200, 2, 123 * BLOCK_SIZE)
 
 
+@pytest.mark.parametrize("io", ["pread", "mmap", "direct"])
+def test_replay_file_io_methods(gpu_ctx, tmp_path, io):
+    """Every input method sees the same bytes: a Zipf image with a ragged
+    tail (not a page multiple, for O_DIRECT's rounded reads) and corruption."""
+    from revel_amd._lib import NOT_SUPPORT
+    rng = np.random.default_rng(61)
+    img = bytearray(oc.write_image(zipf_image(rng, 3 << 20)))
+    img = img[:len(img) - 1234]                  # torn tail inside the last block
+    ref = oc.walk(bytes(img))
+    for v in rng.choice(len(ref) - 1, 5, replace=False):
+        img[int(ref["file_offset"][v]) + 7] ^= 0x20 if ref["length"][v] else 0
+    img = bytes(img)
+    want = oc.walk(img)
+    path = str(tmp_path / "000009.log")
+    with open(path, "wb") as f:
+        f.write(img)
+    bad = want["status"] != 0
+    for off, win, th in [(0, 16 * BLOCK_SIZE, 3), (5 * BLOCK_SIZE, 7 * BLOCK_SIZE, 1), (0, 64 << 20, 8)]:
+        try:
+            st = gpu_ctx.replay_file(path, offset=off, window_bytes=win, io_threads=th, io=io)
+        except RevelError as e:
+            assert io == "direct" and e.code == NOT_SUPPORT  # file system refuses O_DIRECT: loud, not silent
+            pytest.skip("O_DIRECT refused by this file system")
+        sel = want["file_offset"] >= off
+        assert st["bytes"] == len(img) - off
+        assert st["units"] == int(sel.sum()) and st["bad"] == int((bad & sel).sum())
+        first_bad = int(want["file_offset"][bad & sel].min()) if (bad & sel).any() else 2**64 - 1
+        assert st["first_bad_offset"] == first_bad
+
+
 # ---- device append framing (batch add_record) vs the oracle writer ----
 @pytest.mark.parametrize("block_offset", [0, 1, 6, 7, 100, 32760, 32761, 32762, 32767, 32768])
 def test_append_records_matches_writer(gpu_ctx, block_offset):

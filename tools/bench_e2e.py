@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--window-mib", type=int, default=64)
     ap.add_argument("--nbuf", type=int, default=4)
     ap.add_argument("--threads", default="4,8,16")
+    ap.add_argument("--io", default="mmap", help="file input methods: mmap,pread,direct")
     a = ap.parse_args()
     ctx = gpu.GpuContext(0)
     t0 = time.time()
@@ -62,13 +63,15 @@ def main():
         with open(a.path, "wb") as f:
             f.write(memoryview(img))
         del img
-    for th in [int(t) for t in a.threads.split(",")]:
+    runs = [(th, io) for io in (a.io.split(",") if a.source == "file" else ["-"]) for th in
+            [int(t) for t in a.threads.split(",")]]
+    for th, io in runs:
         kw = dict(full_blocks=a.mode == "full", window_bytes=a.window_mib << 20, nbuffers=a.nbuf, io_threads=th)
-        st = ctx.replay_memory(img, **kw) if a.source == "memory" else ctx.replay_file(a.path, **kw)
+        st = ctx.replay_memory(img, **kw) if a.source == "memory" else ctx.replay_file(a.path, io=io, **kw)
         gib = st["bytes"] / 2**30
         print(json.dumps({
             "workload": f"C5 end-to-end replay, {a.mode} layout, source={a.source}",
-            "GiB": round(gib, 2), "io_threads": th, "window_MiB": a.window_mib, "nbuffers": a.nbuf,
+            "GiB": round(gib, 2), "io": io, "io_threads": th, "window_MiB": a.window_mib, "nbuffers": a.nbuf,
             "end_to_end_GiB_s": round(gib / st["seconds"], 2),
             "h2d_GiB_s": round(gib / (st["h2d_ms"] / 1e3), 2),
             "host_fill_GiB_s": round(gib / st["read_seconds"], 2),
