@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -716,9 +717,15 @@ __global__ void k_init_len_tables() {
     }
 }
 
+// Record k's CRC range is [s, em1 + 1).  A bad header (always the last record
+// of a list: the walk stops there) and the sentinel slot after the last
+// record get s = em1 = 0xFFFF, a range no block position reaches, so lanes
+// advance to the next record with two LDS reads and no bounds checks.
+constexpr uint16_t kNoRange = 0xFFFFu;
 struct VerifyWaveLds2 {
-    uint16_t s[kRecCap2];
-    uint16_t em1[kRecCap2];  // end - 1; s - 1 for a bad header (empty range)
+    uint16_t s[kRecCap2 + 1];
+    uint16_t em1[kRecCap2 + 1];
+    uint16_t off[kRecCap2];  // header offset
     uint32_t acc[kRecCap2];
     uint32_t nrec, more_off;
 };
@@ -734,7 +741,32 @@ __device__ __forceinline__ uint32_t byte_step_s4r(uint32_t state, uint32_t b, La
 // the kernel writes mask(crc32c(type||payload)) into bytes [off, off+4) of
 // each header instead of emitting result records.  `lead` = in-block offset
 // of image byte 0 (a batch appended to a partially written block).
-template <bool FRAME>
+template <int BP>
+__device__ __forceinline__ uint32_t record_raw(uint32_t acc, uint32_t off, uint32_t len) {
+    if constexpr (BP == 0) {
+        return acc;
+    } else {
+        const uint32_t e = off + kHeaderSize + len;
+        return gf_mul(c_inv_pad.v[((e + 3u) & ~3u) - e], acc);
+    }
+}
+
+// Boundary paths (BP) for the 16-B steps that hold a record start or end:
+//   BP_BYTES       exact: bytes past the end absorbed one at a time (v2)
+//   BP_MASK        the word holding the end is absorbed with the bytes past e
+//                  zeroed, so every flush is aligned to E = ceil4(e) (R * x^(8 pad));
+//                  the finalizer multiplies by x^(-8 pad).  Branch-light: one
+//                  masked absorb per word, the flush is the only divergence.
+//   BP_MASK_NOVOTE same as BP_MASK without the wave-uniform interior fast path.
+enum BoundaryPath : int { BP_BYTES = 0, BP_MASK = 1, BP_MASK_NOVOTE = 2 };
+
+// WHICH: 0 = every block; 1 = whole blocks only (plain 16-B loads, no guards:
+// the guarded loads of a partial block raise register pressure for the whole
+// kernel); 2 = only the partial blocks (the first, when the image starts
+// mid-block, and the last), launched as one extra workgroup.
+enum BlockSet : int { BS_ALL = 0, BS_WHOLE = 1, BS_PARTIAL = 2 };
+
+template <bool FRAME, int BP = BP_BYTES, int WHICH = BS_ALL>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -756,12 +788,19 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
     const uint64_t nwaves = gridDim.x * waves_per_wg;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+    const uint64_t niter = WHICH == BS_PARTIAL ? std::min<uint64_t>(2, nblocks) : nblocks;
+    for (uint64_t it = gwave; it < niter; it += nwaves) {
+        const uint64_t b = WHICH == BS_PARTIAL && it == 1 ? nblocks - 1 : it;
         const uint64_t base = b * kBlockSize;  // virtual offset of the block
         const uint8_t* blk = image + base - lead;  // dereferenced only at [lo, bl)
         const uint32_t lo_b = b == 0 ? lead : 0u;
         const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, vbytes - base);
-        const bool full = bl == kBlockSize && lo_b == 0;
+        const bool full = WHICH == BS_WHOLE || (bl == kBlockSize && lo_b == 0);
+        if constexpr (WHICH == BS_WHOLE) {
+            if (bl != kBlockSize || lo_b != 0) continue;
+        } else if constexpr (WHICH == BS_PARTIAL) {
+            if (bl == kBlockSize && lo_b == 0) continue;
+        }
         const uint32_t cs = lane * 512u, ce = cs + 512u;
         uint32_t out_base = FRAME ? 0u : first[b];
         uint32_t walk_from = lo_b;
@@ -785,11 +824,14 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                 for (uint32_t k = lane; k < nlist; k += 64) {
                     const uint32_t e = hlist[b * kListPerBlock + k];
                     const uint32_t off = e & 0xFFFFu, len = e >> 16;
-                    wl.s[k] = (uint16_t)(off + 6);
-                    wl.em1[k] = (uint16_t)(len == 0xFFFFu ? off + 5u : off + kHeaderSize + len - 1u);
+                    const bool bad = len == 0xFFFFu;
+                    wl.off[k] = (uint16_t)off;
+                    wl.s[k] = bad ? kNoRange : (uint16_t)(off + 6);
+                    wl.em1[k] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + len - 1u);
                     wl.acc[k] = 0;
                 }
                 if (lane == 0) {
+                    wl.s[nlist] = wl.em1[nlist] = kNoRange;
                     wl.nrec = nlist;
                     wl.more_off = kNone;
                 }
@@ -799,13 +841,16 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                     if (n == kRecCap2) { cont = off; break; }
                     const Hdr h = read_header_range(blk, off, lo_b, bl);
                     const uint32_t st = classify(h, off, bl);
-                    wl.s[n] = (uint16_t)(off + 6);
-                    wl.em1[n] = (uint16_t)(st == REVEL_REC_OK ? off + kHeaderSize + h.len - 1u : off + 5u);
+                    const bool bad = st != REVEL_REC_OK;
+                    wl.off[n] = (uint16_t)off;
+                    wl.s[n] = bad ? kNoRange : (uint16_t)(off + 6);
+                    wl.em1[n] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
                     wl.acc[n] = 0;
                     ++n;
-                    if (st != REVEL_REC_OK) break;
+                    if (bad) break;
                     off += kHeaderSize + h.len;
                 }
+                wl.s[n] = wl.em1[n] = kNoRange;
                 wl.nrec = n;
                 wl.more_off = cont;
             }
@@ -813,8 +858,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
             const uint32_t nrec = wl.nrec;
             const uint32_t cont = wl.more_off;
             auto load_rec = [&](uint32_t k, uint32_t& s, uint32_t& e) {
-                if (k >= nrec) { s = e = kNone; return; }
-                s = wl.s[k];
+                s = wl.s[k];  // k <= nrec: the sentinel ends every list
                 e = uint32_t(wl.em1[k]) + 1u;
             };
             uint32_t lo = 0, hi = nrec;
@@ -824,7 +868,6 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
             }
             uint32_t r = lo, s, e;
             load_rec(r, s, e);
-            while (r < nrec && s == e) { ++r; load_rec(r, s, e); }
             const bool active = cs < bl && r < nrec && s < ce;
             uint32_t state = 0;
             if (__any(active)) {
@@ -838,8 +881,30 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                         const uint32_t p16 = cs + rr * 128 + j * 16;
                         // don't-care gap before the next record, or strictly inside one
                         const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
-                        if (__all(interior)) {
+                        if (BP != BP_MASK_NOVOTE && __all(interior)) {
                             state = absorb4<TM_S4R>(state, cur[j], L, tab);
+                        } else if constexpr (BP != BP_BYTES) {
+                            const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const uint32_t p = p16 + q * 4u;
+                                // a record starts / ends inside [p, p+4) (at most one of each:
+                                // the next type byte is >= 6 bytes past an end)
+                                // words before the start (header / gap) leave the register at 0,
+                                // so a record starting on a 16-B boundary can take the fast path
+                                const uint32_t ds = s - p, de = e - p - 1u;
+                                const bool pre = s >= p, en_in = de < 4u;
+                                uint32_t keep = ds < 4u ? (0xFFFFFFFFu << (8u * ds)) : (pre ? 0u : 0xFFFFFFFFu);
+                                keep &= en_in ? (0xFFFFFFFFu >> (8u * (3u - de))) : 0xFFFFFFFFu;
+                                state = pre ? 0u : state;
+                                state = absorb<TM_S4R>(state, ws[q] & keep, L, tab);
+                                if (en_in) {
+                                    atomicXor(&wl.acc[r], state);  // = raw * x^(8 (E - e))
+                                    state = 0;
+                                    ++r;
+                                    load_rec(r, s, e);
+                                }
+                            }
                         } else {
                             const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
 #pragma unroll
@@ -866,7 +931,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                                     }
                                     atomicXor(&wl.acc[r], state);
                                     state = 0;
-                                    do { ++r; load_rec(r, s, e); } while (r < nrec && s == e);
+                                    ++r;
+                                    load_rec(r, s, e);
                                 }
                             }
                         }
@@ -876,17 +942,20 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                     for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
                 }
                 // record still open at the chunk end: shift its partial register to e
-                if (cs < bl && r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[e - ce], state));
+                if (cs < bl && r < nrec && s < ce && e > ce) {
+                    const uint32_t to = BP == BP_BYTES ? e : (e + 3u) & ~3u;
+                    atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[to - ce], state));
+                }
             }
             have_round0 = false;
             wave_lds_sync();
             for (uint32_t k = lane; k < nrec; k += 64) {
-                const uint32_t off = uint32_t(wl.s[k]) - 6u;
+                const uint32_t off = wl.off[k];
                 const Hdr h = read_header_range(blk, off, lo_b, bl);
                 const uint32_t st = classify(h, off, bl);
                 if constexpr (FRAME) {
                     if (st == REVEL_REC_OK) {
-                        const uint32_t m = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                        const uint32_t m = mask(record_raw<BP>(wl.acc[k], off, h.len) ^ g_init_xor_tab[h.len + 1u]);
                         uint8_t* hp = const_cast<uint8_t*>(blk) + off;
                         hp[0] = (uint8_t)m;
                         hp[1] = (uint8_t)(m >> 8);
@@ -901,7 +970,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                     res.type = (uint8_t)h.type;
                     res.reserved[0] = res.reserved[1] = 0;
                     if (st == REVEL_REC_OK) {
-                        res.computed_crc = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                        res.computed_crc = mask(record_raw<BP>(wl.acc[k], off, h.len) ^ g_init_xor_tab[h.len + 1u]);
                         res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
                     } else {
                         res.computed_crc = 0;
@@ -1537,6 +1606,21 @@ static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
     return hipSuccess;
 }
 
+// Whole blocks on `grid` workgroups, then (only if there is one) the partial
+// first/last block on one more workgroup, same stream.
+template <bool FRAME, int BP>
+static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
+                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                 uint32_t lead, const uint32_t* hl, const uint32_t* d_counts, hipStream_t st) {
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_WHOLE>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
+                       img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !partial) return e;
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img, nbytes,
+                       base_offset, d_first, d_out, lead, hl, d_counts);
+    return hipGetLastError();
+}
+
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                   const uint32_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
@@ -1553,10 +1637,21 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
     if (e0 != hipSuccess) return e0;
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
-    hipLaunchKernelGGL(k_verify_records2<false>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out, 0u,
-                       variant == 2 ? nullptr : d_hlist, d_counts);
-    return hipGetLastError();
+    const uint32_t* hl = variant == 2 ? nullptr : d_hlist;
+    const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    const bool partial = nbytes % kBlockSize != 0;
+    switch (variant) {
+        case 3: return launch_verify2<false, BP_MASK>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                      d_counts, st);
+        case 4: return launch_verify2<false, BP_MASK_NOVOTE>(grid, partial, img, nbytes, base_offset, d_first, d_out,
+                                                             0u, hl, d_counts, st);
+        case 5:  // round-1 production: one kernel for whole and partial blocks
+            hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
+                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts);
+            return hipGetLastError();
+        default: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
+                                                        hl, d_counts, st);
+    }
 }
 
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
@@ -1595,9 +1690,9 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const uint64_t nblocks = (image_len + lead + kBlockSize - 1) / kBlockSize;
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
-    hipLaunchKernelGGL(k_verify_records2<true>, dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr, lead, nullptr, nullptr);
-    return hipGetLastError();
+    const bool partial = lead != 0 || (image_len + lead) % kBlockSize != 0;
+    return launch_verify2<true, BP_BYTES>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull,
+                                          nullptr, nullptr, lead, nullptr, nullptr, st);
 }
 
 hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,

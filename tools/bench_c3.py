@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=1 << 30, help="size of the written Zipf image")
     ap.add_argument("--tile", type=int, default=4, help="repeat the image's whole blocks this many times")
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--variants", default="0,2,1")
+    ap.add_argument("--variants", default="0,3,4")
     a = ap.parse_args()
     t0 = time.time()
     img = make_image(a.bytes)
