@@ -118,7 +118,8 @@ void* revel_gpu_context_stream(revel_gpu_context* ctx);
 /* ---- log reader: src/log_reader.rs ------------------------------------- */
 typedef struct revel_log_reader revel_log_reader;
 /* log_reader.rs:62-74 `Reader::new(file, checksum, initial_offset)`.
- * The reader takes ownership of `file` (Box<dyn SequentialFile>).
+ * The reader takes ownership of `file` (Box<dyn SequentialFile>) in every
+ * case: on failure the file has been freed.
  * With checksum != 0 every physical record's CRC is verified ON THE GPU of
  * `gpu` (required: REVEL_NOT_SUPPORT if NULL); with checksum == 0, gpu may
  * be NULL.  `window_bytes` = bytes read + verified per GPU batch (rounded

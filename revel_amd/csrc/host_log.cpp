@@ -550,10 +550,18 @@ extern "C" {
 
 int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t initial_offset, revel_gpu_context* gpu,
                          size_t window_bytes, revel_log_reader** out) {
-    if (!file || !out) return set_error(REVEL_INVALID_ARGUMENT, "null file/out");
+    // the reader owns `file` from here on, also when construction fails
+    // (Reader::new consumes its Box<dyn SequentialFile>, log_reader.rs:62)
+    if (!out) {
+        revel_sequential_file_free(file);
+        return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    }
     *out = nullptr;
-    if (checksum && !gpu)
+    if (!file) return set_error(REVEL_INVALID_ARGUMENT, "null file");
+    if (checksum && !gpu) {
+        revel_sequential_file_free(file);
         return set_error(REVEL_NOT_SUPPORT, "checksum verification runs on the GPU: pass a revel_gpu_context");
+    }
     auto* r = new revel_log_reader;
     r->file = file;
     r->checksum = checksum != 0;

@@ -51,11 +51,9 @@ class Reader:
         self._gpu = gpu  # keep the context alive
         h = c_void_p()
         fh = file.take()
-        rc = lib().revel_log_reader_new(fh, 1 if checksum else 0, initial_offset,
-                                        gpu.handle if gpu is not None else None, window_bytes, ctypes.byref(h))
-        if rc != 0:
-            lib().revel_sequential_file_free(fh)
-        check(rc)
+        # the reader owns the file from here on, also when construction fails
+        check(lib().revel_log_reader_new(fh, 1 if checksum else 0, initial_offset,
+                                         gpu.handle if gpu is not None else None, window_bytes, ctypes.byref(h)))
         self._h = h.value
 
     def read_record(self) -> Optional[bytes]:

@@ -52,16 +52,25 @@ def main():
     ap.add_argument("--tile", type=int, default=4, help="repeat the image's whole blocks this many times")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--variants", default="0,3,4")
+    ap.add_argument("--image", choices=["zipf", "full"], default="zipf",
+                    help="full = C2-style full blocks (1 record/block): the verify kernels' base cost")
     a = ap.parse_args()
     t0 = time.time()
-    img = make_image(a.bytes)
-    if a.tile > 1:  # whole blocks only, so the tiles stay block-aligned
-        whole = len(img) // BLOCK_SIZE * BLOCK_SIZE
-        img = img[:whole] * a.tile
-    t_write = time.time() - t0
-    n = len(img)
     ctx = gpu.GpuContext(0)
-    d = ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    if a.image == "full":
+        nb = a.bytes * max(1, a.tile) // BLOCK_SIZE
+        n = nb * BLOCK_SIZE
+        d = ctx.alloc(n)
+        check(lib().revel_gpu_synth_full_blocks(ctx.handle, d.ptr, nb, 0x5EED0002, 0, None))
+        ctx.sync()
+    else:
+        img = make_image(a.bytes)
+        if a.tile > 1:  # whole blocks only, so the tiles stay block-aligned
+            whole = len(img) // BLOCK_SIZE * BLOCK_SIZE
+            img = img[:whole] * a.tile
+        n = len(img)
+        d = ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    t_write = time.time() - t0
     res = ctx.verify_image(d, n)
     nrec = len(res)
     bad = int((res["status"] != 0).sum())
@@ -87,7 +96,8 @@ def main():
         same = bool(np.array_equal(got, res))
         ta, tv = float(np.median(times_all)), float(np.median(times_verify))
         print(json.dumps({
-            "workload": "C3 zipf 64B-32KiB records (1 GiB written by the host writer, whole blocks tiled), device walk + segmented CRC verify",
+            "workload": ("C3 zipf 64B-32KiB records (1 GiB written by the host writer, whole blocks tiled), device walk + segmented CRC verify"
+                         if a.image == "zipf" else "C2-layout full blocks through the C3 verify path"),
             "verify_variant": variant, "matches_production": same,
             "image_bytes": n, "blocks": nblocks, "physical_records": nrec, "bad_records": bad,
             "types": {int(t): int((res["type"] == t).sum()) for t in (1, 2, 3, 4)},
