@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
     ap.add_argument("--e2e-gib", type=float, default=4.0,
                     help="per-rank host-RAM replay size for the end_to_end field (0 = skip)")
+    ap.add_argument("--c3-gib", type=float, default=4.0,
+                    help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
     return ap.parse_args()
 
 
@@ -190,6 +192,65 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
     }
 
 
+def c3_records(ctx, D, gib: float, iters: int = 5):
+    """Config C3 on every rank: Zipf(1.1) record sizes 64*k, k in [1, 512]
+    (seed 0x5EED0003 ^ rank), framed ON DEVICE by revel_gpu_append_records
+    (bit-exact with log::Writer, tests/test_gpu.py) from device-generated
+    payload bytes, then the production verify path (count -> scan -> verify)
+    timed with HIP events; all ranks start together, rate = total bytes /
+    max-over-ranks median time."""
+    import numpy as np
+    from revel_amd._lib import check, lib
+    from revel_amd.gpu import RECORD_DTYPE
+    L = lib()
+    rng = np.random.default_rng(0x5EED0003 ^ D.rank)
+    k = np.arange(1, 513)
+    p = k ** -1.1
+    p /= p.sum()
+    target = int(gib * (1 << 30))
+    sizes = (64 * rng.choice(k, size=target // 3000 + 4096, p=p)).astype(np.uint64)
+    sizes = sizes[:int(np.searchsorted(np.cumsum(sizes + 7), target))]
+    nb_pay = (int(sizes.sum()) + BLOCK_SIZE - 1) // BLOCK_SIZE
+    pay = ctx.alloc(nb_pay * BLOCK_SIZE)
+    ctx.synth_full_blocks(pay, nb_pay, seed=0x5EED0003 ^ D.rank)
+    img, n, _ = ctx.append_records(pay, sizes)
+    pay.free()
+    nblocks = (n + BLOCK_SIZE - 1) // BLOCK_SIZE
+    counts, first = ctx.alloc(4 * nblocks), ctx.alloc(4 * nblocks)
+    cap = len(sizes) + 2 * nblocks + 64           # records + FIRST/MIDDLE/LAST splits
+    out = ctx.alloc(cap * RECORD_DTYPE.itemsize)
+    e0, e1 = ctx.event(), ctx.event()
+    times = []
+    D.barrier()
+    for _ in range(iters):
+        e0.record()
+        check(L.revel_gpu_count_records(ctx.handle, img.ptr, n, counts.ptr, None))
+        check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+        check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, out.ptr, None))
+        e1.record()
+        ctx.sync()
+        times.append(e0.elapsed_ms(e1))
+    D.barrier()
+    nphys = int(ctx.d2h(first, 4 * nblocks, np.uint32)[-1]) + int(ctx.d2h(counts, 4 * nblocks, np.uint32)[-1])
+    res = ctx.d2h(out, nphys * RECORD_DTYPE.itemsize).view(RECORD_DTYPE)
+    bad = D.sum(float((res["status"] != 0).sum()))
+    ms = float(np.median(times))
+    ms_max = D.max(ms)
+    for b in (img, counts, first, out):
+        b.free()
+    return {
+        "unit": "GiB/s",
+        "value": round(n * D.world / 2**30 / (ms_max / 1e3), 1),
+        "ms": round(ms_max, 4),
+        "per_rank_bytes": n,
+        "physical_records_rank0": nphys,
+        "bad_records": int(bad),
+        "alg_GB_s_rank0": round((n + 24 * nphys) / (ms / 1e3) / 1e9, 1),
+        "path": "count (per-block header walk + header list) -> scan -> verify (production kernels)",
+        "data": "Zipf(1.1) 64 B..32 KiB records framed on device by revel_gpu_append_records",
+    }
+
+
 def main():
     args = parse()
     D = Dist()
@@ -239,6 +300,10 @@ def main():
     if args.e2e_gib > 0:
         e2e = end_to_end(ctx, D, dblocks, n, args.e2e_gib)
 
+    c3 = None
+    if args.c3_gib > 0:
+        c3 = c3_records(ctx, D, args.c3_gib)
+
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(ctx, dblocks, masked, n, args.cpu_seconds)
@@ -278,6 +343,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "c3": c3,
         }
         print(json.dumps(out), flush=True)
     D.close()

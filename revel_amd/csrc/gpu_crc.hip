@@ -996,7 +996,10 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
 // finalized, so a block no longer pays three global round trips in series.
 // Partial blocks (first/last) still go through k_verify_records2<.., BS_PARTIAL>.
 // ---------------------------------------------------------------------------
-template <bool FRAME>
+// DIAG (experiments only, never production): bit 1 = rounds fully unrolled,
+// bit 2 = no wave vote (every segment takes the fast path: WRONG CRCs, timing
+// only), bit 4 = no finalize (timing only).
+template <bool FRAME, int DIAG = 0>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -1100,7 +1103,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             uint32_t state = 0;
             if (__any(active)) {
                 if (!have_round0) load_round(blk, cur, 0);
-#pragma unroll 1
+#pragma unroll((DIAG & 1) ? 4 : 1)
                 for (int rr = 0; rr < 4; ++rr) {
                     if (rr < 3) load_round(blk, nxt, rr + 1);
                     __builtin_amdgcn_sched_barrier(0);
@@ -1109,7 +1112,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                         const uint32_t p16 = cs + rr * 128 + j * 16;
                         // don't-care gap before the next record, or strictly inside one
                         const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
-                        if (__all(interior)) {
+                        if ((DIAG & 2) || __all(interior)) {
                             state = absorb4<TM_S4R>(state, cur[j], L, tab);
                         } else {
                             const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
@@ -1157,7 +1160,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             const uint32_t off0 = f0 ? uint32_t(wl.off[lane]) : 0u;
             const Hdr h0 = read_header(blk, off0, kBlockSize);
             if (cont == kNone && bn < b_hi) prefetch(bn);
-            for (uint32_t k = lane; k < nrec; k += 64) {
+            for (uint32_t k = lane; k < ((DIAG & 4) ? 0u : nrec); k += 64) {
                 const uint32_t off = k == lane ? off0 : uint32_t(wl.off[k]);
                 const Hdr h = k == lane ? h0 : read_header(blk, off, kBlockSize);
                 const uint32_t st = classify(h, off, kBlockSize);
@@ -1818,11 +1821,11 @@ static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
 // Whole blocks on `grid` workgroups, then (only if there is one) the partial
 // first/last block on one more workgroup, same stream.
 // Production: pipelined whole-block kernel + the partial blocks on one workgroup.
-template <bool FRAME>
+template <bool FRAME, int DIAG = 0>
 static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                  uint32_t lead, const uint32_t* hl, const uint32_t* d_counts, hipStream_t st) {
-    hipLaunchKernelGGL((k_verify_records3<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
+    hipLaunchKernelGGL((k_verify_records3<FRAME, DIAG>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !partial) return e;
@@ -1872,6 +1875,14 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts);
             return hipGetLastError();
+        case 21: return launch_verify3<false, 1>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                 d_counts, st);
+        case 22: return launch_verify3<false, 2>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                 d_counts, st);
+        case 23: return launch_verify3<false, 4>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                 d_counts, st);
+        case 24: return launch_verify3<false, 6>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                 d_counts, st);
         case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
                                                        hl, d_counts, st);
         default: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
