@@ -439,11 +439,32 @@ __device__ __forceinline__ uint32_t classify(const Hdr& h, uint32_t off, uint32_
     return REVEL_REC_OK;
 }
 
+// Header-list entry: the 7 header bytes as read (stored CRC | len << 32 |
+// type << 48).  Offsets are not stored: entry k sits at the sum of 7 + len of
+// the entries before it (a wave prefix sum in the consumer).
+__device__ __forceinline__ uint64_t list_entry(const Hdr& h) {
+    return uint64_t(h.stored) | (uint64_t(h.len | (h.type << 16)) << 32);
+}
+__device__ __forceinline__ Hdr list_header(uint64_t e) {
+    const uint32_t hi = uint32_t(e >> 32);
+    return {uint32_t(e), hi & 0xFFFFu, (hi >> 16) & 0xFFu};
+}
+// Wave-wide exclusive prefix sum (lanes >= n contribute 0).
+__device__ __forceinline__ uint32_t wave_exclusive_sum(uint32_t v) {
+    uint32_t incl = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        incl += lane_id() >= d ? t : 0u;
+    }
+    return incl - v;
+}
+
 // Per block (one lane each): number of physical records and, when list is
-// non-null, the first kListPerBlock headers as (offset | len << 16), len =
-// 0xFFFF marking a bad header (zero record / length past the block).
+// non-null, the first kListPerBlock headers (list_entry; the walk stops at the
+// first bad header, so only the last entry can be bad).
 __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts,
-                                uint32_t* __restrict__ hlist) {
+                                uint64_t* __restrict__ hlist) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
          b += (uint64_t)gridDim.x * blockDim.x) {
@@ -454,7 +475,7 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
         while (bl - off >= kHeaderSize) {
             const Hdr h = read_header(blk, off, bl);
             const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-            if (hlist && n < kListPerBlock) hlist[b * kListPerBlock + n] = off | ((ok ? h.len : 0xFFFFu) << 16);
+            if (hlist && n < kListPerBlock) hlist[b * kListPerBlock + n] = list_entry(h);
             ++n;
             if (!ok) break;
             off += kHeaderSize + h.len;
@@ -727,6 +748,8 @@ struct VerifyWaveLds2 {
     uint16_t em1[kRecCap2 + 1];
     uint16_t off[kRecCap2];  // header offset
     uint32_t acc[kRecCap2];
+    uint32_t hstored[kListPerBlock];  // headers of a list-built batch (v3/v4 finalize)
+    uint32_t hlt[kListPerBlock];      // len | type << 16
     uint32_t nrec, more_off;
 };
 
@@ -772,7 +795,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                                                                      const uint32_t* __restrict__ first,
                                                                      revel_record_result* __restrict__ out,
                                                                      uint32_t lead,
-                                                                     const uint32_t* __restrict__ hlist,
+                                                                     const uint64_t* __restrict__ hlist,
                                                                      const uint32_t* __restrict__ counts) {
     __shared__ uint32_t tab[32768];
     __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
@@ -821,14 +844,14 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
         const uint32_t nlist = (hlist && counts) ? counts[b] : kNone;
         for (;;) {
             if (walk_from == lo_b && nlist <= kListPerBlock) {
-                for (uint32_t k = lane; k < nlist; k += 64) {
-                    const uint32_t e = hlist[b * kListPerBlock + k];
-                    const uint32_t off = e & 0xFFFFu, len = e >> 16;
-                    const bool bad = len == 0xFFFFu;
-                    wl.off[k] = (uint16_t)off;
-                    wl.s[k] = bad ? kNoRange : (uint16_t)(off + 6);
-                    wl.em1[k] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + len - 1u);
-                    wl.acc[k] = 0;
+                const Hdr h = list_header(lane < nlist ? hlist[b * kListPerBlock + lane] : 0ull);
+                const uint32_t off = lo_b + wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
+                if (lane < nlist) {
+                    const bool bad = classify(h, off, bl) != REVEL_REC_OK;
+                    wl.off[lane] = (uint16_t)off;
+                    wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
+                    wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
+                    wl.acc[lane] = 0;
                 }
                 if (lane == 0) {
                     wl.s[nlist] = wl.em1[nlist] = kNoRange;
@@ -1005,7 +1028,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                                                                      const uint32_t* __restrict__ first,
                                                                      revel_record_result* __restrict__ out,
                                                                      uint32_t lead,
-                                                                     const uint32_t* __restrict__ hlist,
+                                                                     const uint64_t* __restrict__ hlist,
                                                                      const uint32_t* __restrict__ counts) {
     __shared__ uint32_t tab[32768];
     __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
@@ -1028,7 +1051,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     uint64_t b = b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
     if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
     uint4 cur[8], nxt[8];
-    uint32_t pf_count = kNone, pf_hl = 0, pf_first = 0;
+    uint32_t pf_count = kNone, pf_first = 0;
+    uint64_t pf_hl = 0;
     auto load_round = [&](const uint8_t* blk, uint4* v, int rr) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + rr * 128 + j * 16));
@@ -1047,19 +1071,26 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
         const uint64_t base = b * kBlockSize;
         const uint8_t* blk = image + base - lead;
         const uint64_t bn = b + nwaves;
-        const uint32_t nlist = pf_count, hl_e = pf_hl;
+        const uint32_t nlist = pf_count;
+        const uint64_t hl_e = pf_hl;
         uint32_t out_base = pf_first;
         uint32_t walk_from = 0;
         bool have_round0 = true;
         for (;;) {
-            if (walk_from == 0 && nlist <= kListPerBlock) {
+            const bool from_list = walk_from == 0 && nlist <= kListPerBlock;
+            if (from_list) {
+                // headers come from the count pass; offsets by prefix sum; the
+                // finalizer reads them back from LDS (no global header reads)
+                const Hdr h = list_header(hl_e);
+                const uint32_t off = wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
                 if (lane < nlist) {
-                    const uint32_t off = hl_e & 0xFFFFu, len = hl_e >> 16;
-                    const bool bad = len == 0xFFFFu;
+                    const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
                     wl.off[lane] = (uint16_t)off;
                     wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
-                    wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + len - 1u);
+                    wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
                     wl.acc[lane] = 0;
+                    wl.hstored[lane] = h.stored;
+                    wl.hlt[lane] = h.len | (h.type << 16);
                 }
                 if (lane == 0) {
                     wl.s[nlist] = wl.em1[nlist] = kNoRange;
@@ -1158,9 +1189,227 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             // finalizer headers first, then the next block's loads, then wait
             const bool f0 = lane < nrec;
             const uint32_t off0 = f0 ? uint32_t(wl.off[lane]) : 0u;
-            const Hdr h0 = read_header(blk, off0, kBlockSize);
+            const Hdr h0 = from_list ? Hdr{wl.hstored[lane & (kListPerBlock - 1)], wl.hlt[lane & (kListPerBlock - 1)] & 0xFFFFu,
+                                           wl.hlt[lane & (kListPerBlock - 1)] >> 16}
+                                     : read_header(blk, off0, kBlockSize);
             if (cont == kNone && bn < b_hi) prefetch(bn);
             for (uint32_t k = lane; k < ((DIAG & 4) ? 0u : nrec); k += 64) {
+                const uint32_t off = k == lane ? off0 : uint32_t(wl.off[k]);
+                const Hdr h = k == lane ? h0 : read_header(blk, off, kBlockSize);
+                const uint32_t st = classify(h, off, kBlockSize);
+                if constexpr (FRAME) {
+                    if (st == REVEL_REC_OK) {
+                        const uint32_t m = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                        uint8_t* hp = const_cast<uint8_t*>(blk) + off;
+                        hp[0] = (uint8_t)m;
+                        hp[1] = (uint8_t)(m >> 8);
+                        hp[2] = (uint8_t)(m >> 16);
+                        hp[3] = (uint8_t)(m >> 24);
+                    }
+                } else {
+                    revel_record_result res;
+                    res.file_offset = base_offset + base - lead + off;
+                    res.length = h.len;
+                    res.stored_crc = h.stored;
+                    res.type = (uint8_t)h.type;
+                    res.reserved[0] = res.reserved[1] = 0;
+                    if (st == REVEL_REC_OK) {
+                        res.computed_crc = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
+                        res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
+                    } else {
+                        res.computed_crc = 0;
+                        res.status = (uint8_t)st;
+                    }
+                    out[out_base + k] = res;
+                }
+            }
+            out_base += nrec;
+            wave_lds_sync();
+            if (cont == kNone) break;
+            walk_from = cont;
+        }
+        b = bn;
+    }
+}
+
+// v4: v3 with a one-compare fast-path test.  Each lane keeps
+//   rel = lim - (cs + 16),  lim = s while the record has not started, else e - 1,
+// so segment j of round rr is interior iff rel >= 16 (8 rr + j) -- one v_cmp
+// against an immediate, then the wave vote.  rel changes only in the slow path.
+template <bool FRAME>
+__global__ __launch_bounds__(kVerify2Threads) void k_verify_records4(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                                                     uint64_t base_offset,
+                                                                     const uint32_t* __restrict__ first,
+                                                                     revel_record_result* __restrict__ out,
+                                                                     uint32_t lead,
+                                                                     const uint64_t* __restrict__ hlist,
+                                                                     const uint32_t* __restrict__ counts) {
+    __shared__ uint32_t tab[32768];
+    __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
+    fill_tables<TM_S4R>(tab);
+    __syncthreads();
+    VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
+    const LaneConst L = make_lane_const();
+    const uint32_t lane = lane_id();
+    const uint64_t vbytes = nbytes + lead;
+    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;  // whole blocks [b_lo, b_hi)
+    const uint64_t waves_per_wg = kVerify2Threads / 64;
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const bool use_list = hlist != nullptr && counts != nullptr;
+    const uint32_t cs = lane * 512u, ce = cs + 512u;
+
+    // wave-uniform block index (readfirstlane: the compiler cannot prove that
+    // threadIdx.x >> 6 is uniform, and would keep the block arithmetic in VGPRs)
+    const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t b = b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
+    if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
+    uint4 cur[8], nxt[8];
+    uint32_t pf_count = kNone, pf_first = 0;
+    uint64_t pf_hl = 0;
+    auto load_round = [&](const uint8_t* blk, uint4* v, int rr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + rr * 128 + j * 16));
+    };
+    // header list first: the list is needed before the data (loads return in order)
+    auto prefetch = [&](uint64_t nb) {
+        if (use_list) {
+            pf_count = counts[nb];
+            pf_hl = hlist[nb * kListPerBlock + lane];
+        }
+        if constexpr (!FRAME) pf_first = first[nb];
+        load_round(image + nb * kBlockSize - lead, cur, 0);
+    };
+    prefetch(b);
+    while (b < b_hi) {
+        const uint64_t base = b * kBlockSize;
+        const uint8_t* blk = image + base - lead;
+        const uint64_t bn = b + nwaves;
+        const uint32_t nlist = pf_count;
+        const uint64_t hl_e = pf_hl;
+        uint32_t out_base = pf_first;
+        uint32_t walk_from = 0;
+        bool have_round0 = true;
+        for (;;) {
+            const bool from_list = walk_from == 0 && nlist <= kListPerBlock;
+            if (from_list) {
+                // headers come from the count pass; offsets by prefix sum; the
+                // finalizer reads them back from LDS (no global header reads)
+                const Hdr h = list_header(hl_e);
+                const uint32_t off = wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
+                if (lane < nlist) {
+                    const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
+                    wl.off[lane] = (uint16_t)off;
+                    wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
+                    wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
+                    wl.acc[lane] = 0;
+                    wl.hstored[lane] = h.stored;
+                    wl.hlt[lane] = h.len | (h.type << 16);
+                }
+                if (lane == 0) {
+                    wl.s[nlist] = wl.em1[nlist] = kNoRange;
+                    wl.nrec = nlist;
+                    wl.more_off = kNone;
+                }
+            } else if (lane == 0) {
+                uint32_t off = walk_from, n = 0, cont = kNone;
+                while (kBlockSize - off >= kHeaderSize) {
+                    if (n == kRecCap2) { cont = off; break; }
+                    const Hdr h = read_header(blk, off, kBlockSize);
+                    const uint32_t st = classify(h, off, kBlockSize);
+                    const bool bad = st != REVEL_REC_OK;
+                    wl.off[n] = (uint16_t)off;
+                    wl.s[n] = bad ? kNoRange : (uint16_t)(off + 6);
+                    wl.em1[n] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
+                    wl.acc[n] = 0;
+                    ++n;
+                    if (bad) break;
+                    off += kHeaderSize + h.len;
+                }
+                wl.s[n] = wl.em1[n] = kNoRange;
+                wl.nrec = n;
+                wl.more_off = cont;
+            }
+            wave_lds_sync();
+            const uint32_t nrec = wl.nrec;
+            const uint32_t cont = wl.more_off;
+            auto load_rec = [&](uint32_t k, uint32_t& s, uint32_t& e) {
+                s = wl.s[k];  // k <= nrec: the sentinel ends every list
+                e = uint32_t(wl.em1[k]) + 1u;
+            };
+            uint32_t lo = 0, hi = nrec;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
+            }
+            uint32_t r = lo, s, e;
+            load_rec(r, s, e);
+            const bool active = r < nrec && s < ce;
+            uint32_t state = 0;
+            int32_t rel = int32_t(s >= cs ? s : e - 1u) - int32_t(cs + 16u);
+            if (__any(active)) {
+                if (!have_round0) load_round(blk, cur, 0);
+#pragma unroll 1
+                for (int rr = 0; rr < 4; ++rr) {
+                    if (rr < 3) load_round(blk, nxt, rr + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t p16 = cs + rr * 128 + j * 16;
+                        // don't-care gap before the next record, or strictly inside one
+                        if (__all(rel >= rr * 128 + j * 16)) {
+                            state = absorb4<TM_S4R>(state, cur[j], L, tab);
+                        } else {
+                            const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const uint32_t p = p16 + q * 4u;
+                                const uint32_t w = ws[q];
+                                if (s >= p + 4u) {
+                                    // gap word (or no record left): state is don't-care
+                                } else if (e > p + 4u) {
+                                    // record continues past this word; maybe starts in it
+                                    if (s >= p) state = 0;
+                                    const uint32_t lb = s > p ? s - p : 0u;
+                                    state = absorb<TM_S4R>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
+                                } else if (e > p) {
+                                    // record ends in this word (and may start in it)
+                                    if (s >= p) state = 0;
+                                    const uint32_t lb = s > p ? s - p : 0u;
+                                    const uint32_t hb = e - p;
+                                    if (lb == 0 && hb == 4) {
+                                        state = absorb<TM_S4R>(state, w, L, tab);
+                                    } else {
+                                        for (uint32_t t = lb; t < hb; ++t)
+                                            state = byte_step_s4r(state, (w >> (8u * t)) & 0xffu, L, tab);
+                                    }
+                                    atomicXor(&wl.acc[r], state);
+                                    state = 0;
+                                    ++r;
+                                    load_rec(r, s, e);
+                                }
+                            }
+                            const uint32_t pn = p16 + 16u;  // the next segment
+                            rel = int32_t(s >= pn ? s : e - 1u) - int32_t(cs + 16u);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+                }
+                // record still open at the chunk end: shift its partial register to e
+                if (r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[e - ce], state));
+            }
+            have_round0 = false;
+            wave_lds_sync();
+            // finalizer headers first, then the next block's loads, then wait
+            const bool f0 = lane < nrec;
+            const uint32_t off0 = f0 ? uint32_t(wl.off[lane]) : 0u;
+            const Hdr h0 = from_list ? Hdr{wl.hstored[lane & (kListPerBlock - 1)], wl.hlt[lane & (kListPerBlock - 1)] & 0xFFFFu,
+                                           wl.hlt[lane & (kListPerBlock - 1)] >> 16}
+                                     : read_header(blk, off0, kBlockSize);
+            if (cont == kNone && bn < b_hi) prefetch(bn);
+            for (uint32_t k = lane; k < nrec; k += 64) {
                 const uint32_t off = k == lane ? off0 : uint32_t(wl.off[k]);
                 const Hdr h = k == lane ? h0 : read_header(blk, off, kBlockSize);
                 const uint32_t st = classify(h, off, kBlockSize);
@@ -1774,7 +2023,7 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 }
 
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                         uint32_t* d_hlist, hipStream_t st) {
+                         uint64_t* d_hlist, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     // one lane per block: every header chain walks concurrently
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
@@ -1820,11 +2069,24 @@ static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
 
 // Whole blocks on `grid` workgroups, then (only if there is one) the partial
 // first/last block on one more workgroup, same stream.
+template <bool FRAME>
+static hipError_t launch_verify4(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
+                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
+    hipLaunchKernelGGL((k_verify_records4<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
+                       base_offset, d_first, d_out, lead, hl, d_counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !partial) return e;
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img,
+                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
+    return hipGetLastError();
+}
+
 // Production: pipelined whole-block kernel + the partial blocks on one workgroup.
 template <bool FRAME, int DIAG = 0>
 static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                 uint32_t lead, const uint32_t* hl, const uint32_t* d_counts, hipStream_t st) {
+                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
     hipLaunchKernelGGL((k_verify_records3<FRAME, DIAG>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
@@ -1837,7 +2099,7 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
 template <bool FRAME, int BP>
 static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                 uint32_t lead, const uint32_t* hl, const uint32_t* d_counts, hipStream_t st) {
+                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_WHOLE>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
                        img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
@@ -1849,7 +2111,7 @@ static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img
 
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                  const uint32_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
+                                  const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (variant == 1) {
         const uint64_t waves = kVerifyThreads / 64;
@@ -1863,7 +2125,7 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
     if (e0 != hipSuccess) return e0;
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
-    const uint32_t* hl = variant == 2 ? nullptr : d_hlist;
+    const uint64_t* hl = variant == 2 ? nullptr : d_hlist;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
     const bool partial = nbytes % kBlockSize != 0;
     switch (variant) {
@@ -1875,6 +2137,8 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts);
             return hipGetLastError();
+        case 8: return launch_verify4<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                             d_counts, st);
         case 21: return launch_verify3<false, 1>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
                                                  d_counts, st);
         case 22: return launch_verify3<false, 2>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
@@ -1891,7 +2155,7 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
 }
 
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                          const uint32_t* d_first, revel_record_result* d_out, const uint32_t* d_hlist,
+                          const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                           const uint32_t* d_counts, hipStream_t st) {
     return verify_records_variant(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
 }

@@ -30,10 +30,11 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
 hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st);
 hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
                              hipStream_t st);
-// d_hlist (nullable): nblocks * kListPerBlock u32 header list for verify.
+// d_hlist (nullable): nblocks * kListPerBlock u64 header-list entries for verify
+// (the 7 header bytes of each of a block's first kListPerBlock records).
 constexpr uint32_t kListPerBlock = 64;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                         uint32_t* d_hlist, hipStream_t st);
+                         uint64_t* d_hlist, hipStream_t st);
 // d_tile_scratch: scan_scratch_words(n) u32 of device scratch.
 hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
                               uint32_t* d_tile_scratch, hipStream_t st);
@@ -52,9 +53,9 @@ hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t imag
 // 2 = production kernel forced to walk headers itself.
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                  const uint32_t* d_hlist, const uint32_t* d_counts, hipStream_t st);
+                                  const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st);
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                          const uint32_t* d_first, revel_record_result* d_out, const uint32_t* d_hlist,
+                          const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                           const uint32_t* d_counts, hipStream_t st);
 
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
@@ -101,7 +102,7 @@ struct revel_gpu_context {
     // Header lists written by revel_gpu_count_records for the image it last
     // counted (single-threaded handle, so count -> scan -> verify on the same
     // context reuses them; any other image makes verify walk headers itself).
-    uint32_t* hlist = nullptr;
+    uint64_t* hlist = nullptr;
     uint64_t hlist_cap_blocks = 0;
     const void* hlist_image = nullptr;
     uint64_t hlist_nbytes = 0;

@@ -36,7 +36,7 @@ struct Window {
     void* d = nullptr;             // device window
     uint32_t* d_counts = nullptr;  // RECORDS
     uint32_t* d_first = nullptr;
-    uint32_t* d_hlist = nullptr;
+    uint64_t* d_hlist = nullptr;
     uint32_t* d_scan = nullptr;
     revel_record_result* d_res = nullptr;
     uint32_t* d_masked = nullptr;  // FULL_BLOCKS
@@ -89,7 +89,7 @@ int ring_init(Ring& R, int nbuf) {
         if (R.mode == REVEL_REPLAY_RECORDS) {
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_counts), nblocks * 4), "hipMalloc(counts)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_first), nblocks * 4), "hipMalloc(first)");
-            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), nblocks * revel::kListPerBlock * 4), "hipMalloc(hlist)");
+            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), nblocks * revel::kListPerBlock * 8), "hipMalloc(hlist)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_scan), revel::scan_scratch_words(nblocks) * 4), "hipMalloc(scan)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_res), nblocks * kMaxRecordsPerBlock * sizeof(revel_record_result)),
                 "hipMalloc(records)");
