@@ -760,6 +760,16 @@ __device__ __forceinline__ uint32_t byte_step_s4r(uint32_t state, uint32_t b, La
     return ldsw<128>(tab, a) ^ (state >> 8);
 }
 
+template <int TM>
+__device__ __forceinline__ uint32_t byte_step_tm(uint32_t state, uint32_t b, LaneConst L, const uint32_t* tab) {
+    if constexpr (TM == TM_S4R) {
+        return byte_step_s4r(state, b, L, tab);
+    } else {
+        static_assert(TM == TM_S4, "byte steps: S4R or S4 tables");
+        return tab[768 + ((state ^ b) & 0xffu)] ^ (state >> 8);  // T0 of the [T3|T2|T1|T0] image
+    }
+}
+
 // FRAME = device append framing: headers hold length/type but no CRC yet;
 // the kernel writes mask(crc32c(type||payload)) into bytes [off, off+4) of
 // each header instead of emitting result records.  `lead` = in-block offset
@@ -789,24 +799,24 @@ enum BoundaryPath : int { BP_BYTES = 0, BP_MASK = 1, BP_MASK_NOVOTE = 2 };
 // mid-block, and the last), launched as one extra workgroup.
 enum BlockSet : int { BS_ALL = 0, BS_WHOLE = 1, BS_PARTIAL = 2 };
 
-template <bool FRAME, int BP = BP_BYTES, int WHICH = BS_ALL>
-__global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8_t* __restrict__ image, uint64_t nbytes,
+template <bool FRAME, int BP = BP_BYTES, int WHICH = BS_ALL, int TM = TM_S4R, int THREADS = kVerify2Threads>
+__global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
                                                                      revel_record_result* __restrict__ out,
                                                                      uint32_t lead,
                                                                      const uint64_t* __restrict__ hlist,
                                                                      const uint32_t* __restrict__ counts) {
-    __shared__ uint32_t tab[32768];
-    __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
-    fill_tables<TM_S4R>(tab);
+    __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
+    __shared__ VerifyWaveLds2 wl_all[THREADS / 64];
+    fill_tables<TM>(tab);
     __syncthreads();
     VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
     const LaneConst L = make_lane_const();
     const uint32_t lane = lane_id();
     const uint64_t vbytes = nbytes + lead;  // bytes of the virtual block-aligned image
     const uint64_t nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
-    const uint64_t waves_per_wg = kVerify2Threads / 64;
+    const uint64_t waves_per_wg = THREADS / 64;
     const uint64_t gwave = blockIdx.x * waves_per_wg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nwaves = gridDim.x * waves_per_wg;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -905,7 +915,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                         // don't-care gap before the next record, or strictly inside one
                         const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
                         if (BP != BP_MASK_NOVOTE && __all(interior)) {
-                            state = absorb4<TM_S4R>(state, cur[j], L, tab);
+                            state = absorb4<TM>(state, cur[j], L, tab);
                         } else if constexpr (BP != BP_BYTES) {
                             const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
 #pragma unroll
@@ -920,7 +930,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                                 uint32_t keep = ds < 4u ? (0xFFFFFFFFu << (8u * ds)) : (pre ? 0u : 0xFFFFFFFFu);
                                 keep &= en_in ? (0xFFFFFFFFu >> (8u * (3u - de))) : 0xFFFFFFFFu;
                                 state = pre ? 0u : state;
-                                state = absorb<TM_S4R>(state, ws[q] & keep, L, tab);
+                                state = absorb<TM>(state, ws[q] & keep, L, tab);
                                 if (en_in) {
                                     atomicXor(&wl.acc[r], state);  // = raw * x^(8 (E - e))
                                     state = 0;
@@ -940,17 +950,17 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records2(const uint8
                                     // record continues past this word; maybe starts in it
                                     if (s >= p) state = 0;
                                     const uint32_t lb = s > p ? s - p : 0u;
-                                    state = absorb<TM_S4R>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
+                                    state = absorb<TM>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
                                 } else if (e > p) {
                                     // record ends in this word (and may start in it)
                                     if (s >= p) state = 0;
                                     const uint32_t lb = s > p ? s - p : 0u;
                                     const uint32_t hb = e - p;
                                     if (lb == 0 && hb == 4) {
-                                        state = absorb<TM_S4R>(state, w, L, tab);
+                                        state = absorb<TM>(state, w, L, tab);
                                     } else {
                                         for (uint32_t t = lb; t < hb; ++t)
-                                            state = byte_step_s4r(state, (w >> (8u * t)) & 0xffu, L, tab);
+                                            state = byte_step_tm<TM>(state, (w >> (8u * t)) & 0xffu, L, tab);
                                     }
                                     atomicXor(&wl.acc[r], state);
                                     state = 0;
@@ -2077,7 +2087,9 @@ static hipError_t launch_verify4(uint64_t grid, bool partial, const uint8_t* img
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !partial) return e;
-    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img,
+    // <= 2 partial blocks: one single-wave workgroup each, 4 KiB unreplicated tables
+    // (a 128 KiB table fill and one latency-bound wave cost ~50 us per launch)
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64>), dim3(2), dim3(64), 0, st, img,
                        nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
     return hipGetLastError();
 }
@@ -2091,7 +2103,9 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !partial) return e;
-    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img,
+    // <= 2 partial blocks: one single-wave workgroup each, 4 KiB unreplicated tables
+    // (a 128 KiB table fill and one latency-bound wave cost ~50 us per launch)
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64>), dim3(2), dim3(64), 0, st, img,
                        nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
     return hipGetLastError();
 }
