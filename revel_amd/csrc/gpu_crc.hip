@@ -1144,7 +1144,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             uint32_t state = 0;
             if (__any(active)) {
                 if (!have_round0) load_round(blk, cur, 0);
-#pragma unroll((DIAG & 1) ? 4 : 1)
+                constexpr int kRoundUnroll = (DIAG & 1) ? 4 : 1;
+#pragma unroll kRoundUnroll
                 for (int rr = 0; rr < 4; ++rr) {
                     if (rr < 3) load_round(blk, nxt, rr + 1);
                     __builtin_amdgcn_sched_barrier(0);
@@ -1576,22 +1577,45 @@ __global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint6
     }
 }
 
+// One wave copies len bytes src -> dst, any byte alignment of either: a byte
+// head up to dst's next 16-B boundary, then aligned 16-B stores whose source
+// bytes are funnel-shifted (v_alignbyte) out of 4-B-aligned dword loads (never
+// reading past the source range), then a byte tail.  Coalesced both ways.
+__device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
+    const uint32_t lane = lane_id();
+    const uint32_t head = min(len, (16u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
+    if (lane < head) dst[lane] = src[lane];
+    const uint8_t* s = src + head;
+    uint8_t* d = dst + head;
+    const uint32_t n = len - head;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s - sh);
+    // vector v reads s4[4v .. 4v+3] (+ s4[4v+4] when sh != 0): stay inside [s, s+n)
+    const uint32_t nvec = sh == 0 ? n / 16u : (n + sh >= 20u ? (n + sh - 20u) / 16u + 1u : 0u);
+    for (uint32_t v = lane; v < nvec; v += 64) {
+        const uint32_t* q = s4 + 4u * v;
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = sh ? q[4] : 0u;
+        uint4 o;
+        o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        *reinterpret_cast<uint4*>(d + 16u * v) = o;
+    }
+    for (uint32_t i = nvec * 16u + lane; i < n; i += 64) d[i] = s[i];
+}
+
 // One wave per physical record that belongs to an emitted logical record.
 __global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image_base,
                                const revel_record_result* __restrict__ phys, uint64_t n,
                                const uint64_t* __restrict__ frag_dst, uint8_t* __restrict__ payload) {
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t k = blockIdx.x * (uint64_t)(blockDim.x / 64) + (threadIdx.x >> 6); k < n; k += waves) {
+    const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t k = w0; k < n; k += waves) {
         const uint64_t dst = frag_dst[k];
         if (dst == ~0ull) continue;
         const revel_record_result r = phys[k];
-        const uint8_t* src = image + (r.file_offset - image_base) + kHeaderSize;
-        uint8_t* d = payload + dst;
-        for (uint32_t i = lane_id() * 4; i < r.length; i += 256) {
-#pragma unroll
-            for (uint32_t b = 0; b < 4; ++b)
-                if (i + b < r.length) d[i + b] = src[i + b];
-        }
+        wave_copy(image + (r.file_offset - image_base) + kHeaderSize, payload + dst, r.length);
     }
 }
 

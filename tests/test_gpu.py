@@ -381,6 +381,17 @@ def test_reassemble_golden(gpu_ctx, golden_index, checksum):
         check_reassembly(gpu_ctx, golden_image(name), checksum)
 
 
+def test_reassemble_gather_alignments(gpu_ctx):
+    """Every payload length 0..99 plus 33-B multiples, so fragments start and
+    end at every offset mod 16 in the image and in the gathered buffer."""
+    rng = np.random.default_rng(32)
+    sizes = list(range(100)) + [33 * k for k in range(1, 40)] + [32761, 32762, 40000, 65536]
+    rng.shuffle(sizes)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    for boff in (0, 5):
+        check_reassembly(gpu_ctx, oc.write_image(recs, boff) if boff == 0 else oc.write_image(recs), True)
+
+
 def test_reassemble_mixed_corruption(gpu_ctx):
     rng = np.random.default_rng(31)
     recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 120000, 80)]
