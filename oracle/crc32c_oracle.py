@@ -321,8 +321,16 @@ class LogReader:
         self.checksum = checksum
         self.initial_offset = initial_offset
         self.resyncing = initial_offset > 0
-        self.i = 0
         self._image = image
+        # SkipToInitialBlock (LevelDB; the reference leaves it todo!()): reading
+        # starts at the block holding initial_offset -- or the next one when only
+        # a trailer (< 7 bytes) remains in it -- so records of earlier blocks are
+        # never read, and their corruption never reported.
+        in_block = initial_offset % BLOCK_SIZE
+        start = initial_offset - in_block + (BLOCK_SIZE if in_block > BLOCK_SIZE - 6 else 0)
+        self.i = 0
+        while self.i < len(self.records) and self.records[self.i].file_offset < start:
+            self.i += 1
 
     def read_record(self) -> Optional[bytes]:
         scratch = bytearray()
