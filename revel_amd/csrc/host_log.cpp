@@ -499,6 +499,8 @@ int gpu_verify_window(revel_log_reader* r) {
     if (!rc) rc = revel_gpu_stream_synchronize(g, st);
     if (rc) return rc;
     const size_t total = (size_t)tail[0] + tail[1];
+    r->recs.clear();
+    if (total == 0) return REVEL_OK;  // e.g. only a truncated header at the end of the file
     if (total > r->d_out_cap) {
         if (r->d_out) revel_gpu_free(g, r->d_out);
         r->d_out = nullptr;
@@ -509,7 +511,7 @@ int gpu_verify_window(revel_log_reader* r) {
     }
     r->recs.resize(total);
     rc = revel_gpu_verify_records(g, r->d_win, r->win_len, r->win_file_off, r->d_first, r->d_out, st);
-    if (!rc && total) rc = revel_gpu_memcpy_d2h(g, r->recs.data(), r->d_out, total * sizeof(revel_record_result), st);
+    if (!rc) rc = revel_gpu_memcpy_d2h(g, r->recs.data(), r->d_out, total * sizeof(revel_record_result), st);
     if (!rc) rc = revel_gpu_stream_synchronize(g, st);
     return rc;
 }

@@ -523,3 +523,60 @@ def test_decode_batches_capacity(gpu_ctx):
         check(lib().revel_gpu_decode_batches(gpu_ctx.handle, pay.ptr, pb, out.ptr, nl, info.ptr, ent.ptr, 3,
                                              ctypes.byref(n), None))
     assert n.value == ne
+
+
+def test_gpu_entry_points_on_empty_inputs(gpu_ctx, tmp_path):
+    """Zero-length images, files and record sets: no launch faults, empty results."""
+    d = gpu_ctx.alloc(BLOCK_SIZE)
+    assert len(gpu_ctx.verify_image(d, 0)) == 0
+    ev, payload, phys = gpu_ctx.reassemble(d, 0)
+    assert len(ev) == 0 and len(payload) == 0 and len(phys) == 0
+    ev, payload, infos, ents = gpu_ctx.replay_batches(d, 0)
+    assert len(infos) == 0 and len(ents) == 0
+    path = str(tmp_path / "empty.log")
+    open(path, "wb").close()
+    for io in ("mmap", "pread"):
+        st = gpu_ctx.replay_file(path, io=io)
+        assert (st["bytes"], st["units"], st["bad"]) == (0, 0, 0)
+    st = gpu_ctx.replay_memory(b"")
+    assert (st["bytes"], st["units"]) == (0, 0)
+    assert list(log.Reader(env.MemorySequentialFile(b""), checksum=True, gpu=gpu_ctx)) == []
+    img, n, bo = gpu_ctx.append_records(d, [], block_offset=5)
+    assert (n, bo) == (0, 5)
+    # a lone trailer (< 7 bytes): no records
+    assert len(gpu_ctx.verify_image(gpu_ctx.upload(np.zeros(6, np.uint8)), 6)) == 0
+
+
+def test_property_random_streams_vs_oracle(gpu_ctx):
+    """Hypothesis: random record streams (sizes clustered at the block-edge cases),
+    optional bit flip and truncation -> device walk/verify, reassembly and the
+    GPU reader all equal the oracle."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as hs
+    edge = hs.sampled_from([0, 1, 2, 3, 4, 5, 6, 7, 8, 15, 16, 17, 32754, 32755, 32760, 32761, 32762, 32768, 65522])
+    size = hs.one_of(edge, hs.integers(0, 70000))
+
+    @settings(max_examples=40, deadline=None, suppress_health_check=list(HealthCheck), derandomize=True)
+    @given(sizes=hs.lists(size, min_size=0, max_size=25), seed=hs.integers(0, 2**32 - 1),
+           flip=hs.booleans(), cut=hs.integers(0, 40), off=hs.integers(0, 200000),
+           window=hs.sampled_from([32768, 65536, 1 << 20]))
+    def prop(sizes, seed, flip, cut, off, window):
+        rng = np.random.default_rng(seed)
+        img = bytearray(oc.write_image([rng.integers(0, 256, s, dtype=np.uint8).tobytes() for s in sizes]))
+        if flip and len(img) > 0:
+            img[int(rng.integers(0, len(img)))] ^= 1 << int(rng.integers(0, 8))
+        if cut and len(img) > cut:
+            img = img[:len(img) - cut]
+        img = bytes(img)
+        if img:
+            d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+            compare_walk(gpu_ctx.verify_image(d, len(img)), oc.walk(img))
+            check_reassembly(gpu_ctx, img, True)
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=True, gpu=gpu_ctx, window_bytes=window)
+        assert drain(rd.read_record) == drain(po.LogReader(img, True, 0).read_record)
+        off = min(off, len(img))
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=True, gpu=gpu_ctx, initial_offset=off,
+                        window_bytes=window)
+        assert drain(rd.read_record) == drain(po.LogReader(img, True, off).read_record)
+
+    prop()
