@@ -580,3 +580,28 @@ def test_property_random_streams_vs_oracle(gpu_ctx):
         assert drain(rd.read_record) == drain(po.LogReader(img, True, off).read_record)
 
     prop()
+
+
+def test_property_batch_decode_mutations(gpu_ctx):
+    """Hypothesis: WriteBatch logs whose batch bytes are mutated before framing
+    (valid log records carrying malformed batches) -> device decode == oracle."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as hs
+    from tests_gen import batch_log
+
+    @settings(max_examples=25, deadline=None, suppress_health_check=list(HealthCheck), derandomize=True)
+    @given(seed=hs.integers(0, 2**32 - 1), nb=hs.integers(1, 30), nmut=hs.integers(0, 12),
+           trunc=hs.integers(0, 3))
+    def prop(seed, nb, nmut, trunc):
+        rng = np.random.default_rng(seed)
+        reps = [bytearray(r) for r in batch_log(rng, nb, max_entries=12, max_key=40, max_value=300)]
+        for _ in range(nmut):
+            r = reps[int(rng.integers(0, len(reps)))]
+            if r:
+                r[int(rng.integers(0, len(r)))] = int(rng.integers(0, 256))
+        for _ in range(trunc):
+            k = int(rng.integers(0, len(reps)))
+            reps[k] = reps[k][:int(rng.integers(0, len(reps[k]) + 1))]
+        check_batches(gpu_ctx, oc.write_image([bytes(r) for r in reps]))
+
+    prop()

@@ -180,3 +180,46 @@ def test_framed_size_matches_writer():
         lens = np.array([len(r) for r in recs], dtype=np.uint64)
         n = revel_amd.lib().revel_log_framed_size(lens.ctypes.data, len(lens), boff)
         assert n == len(po.write_image(recs, boff))
+
+
+def test_property_writer_and_host_reader_vs_oracle():
+    """Hypothesis (CPU): product writer at random block offsets == C oracle
+    writer; host-walk reader (checksum off) == oracle LogReader under bit
+    flips, truncation and initial offsets."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as hs
+    edge = hs.sampled_from([0, 1, 6, 7, 8, 32754, 32755, 32760, 32761, 32762, 65522])
+    size = hs.one_of(edge, hs.integers(0, 70000))
+
+    def drain(read_record):
+        out = []
+        for _ in range(100000):
+            try:
+                r = read_record()
+            except (RevelError, po.CorruptionError):
+                out.append("E")
+                continue
+            if r is None:
+                return out
+            out.append(r)
+        raise AssertionError("no EOF")
+
+    @settings(max_examples=60, deadline=None, suppress_health_check=list(HealthCheck), derandomize=True)
+    @given(sizes=hs.lists(size, max_size=20), seed=hs.integers(0, 2**32 - 1), boff=hs.integers(0, 32768),
+           flip=hs.booleans(), cut=hs.integers(0, 40), off=hs.integers(0, 150000),
+           window=hs.sampled_from([32768, 65536, 1 << 20]))
+    def prop(sizes, seed, boff, flip, cut, off, window):
+        rng = np.random.default_rng(seed)
+        recs = [rng.integers(0, 256, s, dtype=np.uint8).tobytes() for s in sizes]
+        assert write_mem(recs, boff) == oc.write_image(recs, boff)
+        img = bytearray(oc.write_image(recs))
+        if flip and img:
+            img[int(rng.integers(0, len(img)))] ^= 1 << int(rng.integers(0, 8))
+        if cut and len(img) > cut:
+            img = img[:len(img) - cut]
+        img = bytes(img)
+        off = min(off, len(img))
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=False, initial_offset=off, window_bytes=window)
+        assert drain(rd.read_record) == drain(po.LogReader(img, False, off).read_record)
+
+    prop()
