@@ -1029,10 +1029,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 // finalized, so a block no longer pays three global round trips in series.
 // Partial blocks (first/last) still go through k_verify_records2<.., BS_PARTIAL>.
 // ---------------------------------------------------------------------------
-// DIAG (experiments only, never production): bit 1 = rounds fully unrolled,
-// bit 2 = no wave vote (every segment takes the fast path: WRONG CRCs, timing
-// only), bit 4 = no finalize (timing only).
-template <bool FRAME, int DIAG = 0>
+template <bool FRAME>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -1144,222 +1141,6 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             uint32_t state = 0;
             if (__any(active)) {
                 if (!have_round0) load_round(blk, cur, 0);
-                constexpr int kRoundUnroll = (DIAG & 1) ? 4 : 1;
-#pragma unroll kRoundUnroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    if (rr < 3) load_round(blk, nxt, rr + 1);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const uint32_t p16 = cs + rr * 128 + j * 16;
-                        // don't-care gap before the next record, or strictly inside one
-                        const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
-                        if ((DIAG & 2) || __all(interior)) {
-                            state = absorb4<TM_S4R>(state, cur[j], L, tab);
-                        } else {
-                            const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const uint32_t p = p16 + q * 4u;
-                                const uint32_t w = ws[q];
-                                if (s >= p + 4u) {
-                                    // gap word (or no record left): state is don't-care
-                                } else if (e > p + 4u) {
-                                    // record continues past this word; maybe starts in it
-                                    if (s >= p) state = 0;
-                                    const uint32_t lb = s > p ? s - p : 0u;
-                                    state = absorb<TM_S4R>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
-                                } else if (e > p) {
-                                    // record ends in this word (and may start in it)
-                                    if (s >= p) state = 0;
-                                    const uint32_t lb = s > p ? s - p : 0u;
-                                    const uint32_t hb = e - p;
-                                    if (lb == 0 && hb == 4) {
-                                        state = absorb<TM_S4R>(state, w, L, tab);
-                                    } else {
-                                        for (uint32_t t = lb; t < hb; ++t)
-                                            state = byte_step_s4r(state, (w >> (8u * t)) & 0xffu, L, tab);
-                                    }
-                                    atomicXor(&wl.acc[r], state);
-                                    state = 0;
-                                    ++r;
-                                    load_rec(r, s, e);
-                                }
-                            }
-                        }
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
-                }
-                // record still open at the chunk end: shift its partial register to e
-                if (r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[e - ce], state));
-            }
-            have_round0 = false;
-            wave_lds_sync();
-            // finalizer headers first, then the next block's loads, then wait
-            const bool f0 = lane < nrec;
-            const uint32_t off0 = f0 ? uint32_t(wl.off[lane]) : 0u;
-            const Hdr h0 = from_list ? Hdr{wl.hstored[lane & (kListPerBlock - 1)], wl.hlt[lane & (kListPerBlock - 1)] & 0xFFFFu,
-                                           wl.hlt[lane & (kListPerBlock - 1)] >> 16}
-                                     : read_header(blk, off0, kBlockSize);
-            if (cont == kNone && bn < b_hi) prefetch(bn);
-            for (uint32_t k = lane; k < ((DIAG & 4) ? 0u : nrec); k += 64) {
-                const uint32_t off = k == lane ? off0 : uint32_t(wl.off[k]);
-                const Hdr h = k == lane ? h0 : read_header(blk, off, kBlockSize);
-                const uint32_t st = classify(h, off, kBlockSize);
-                if constexpr (FRAME) {
-                    if (st == REVEL_REC_OK) {
-                        const uint32_t m = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
-                        uint8_t* hp = const_cast<uint8_t*>(blk) + off;
-                        hp[0] = (uint8_t)m;
-                        hp[1] = (uint8_t)(m >> 8);
-                        hp[2] = (uint8_t)(m >> 16);
-                        hp[3] = (uint8_t)(m >> 24);
-                    }
-                } else {
-                    revel_record_result res;
-                    res.file_offset = base_offset + base - lead + off;
-                    res.length = h.len;
-                    res.stored_crc = h.stored;
-                    res.type = (uint8_t)h.type;
-                    res.reserved[0] = res.reserved[1] = 0;
-                    if (st == REVEL_REC_OK) {
-                        res.computed_crc = mask(wl.acc[k] ^ g_init_xor_tab[h.len + 1u]);
-                        res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
-                    } else {
-                        res.computed_crc = 0;
-                        res.status = (uint8_t)st;
-                    }
-                    out[out_base + k] = res;
-                }
-            }
-            out_base += nrec;
-            wave_lds_sync();
-            if (cont == kNone) break;
-            walk_from = cont;
-        }
-        b = bn;
-    }
-}
-
-// v4: v3 with a one-compare fast-path test.  Each lane keeps
-//   rel = lim - (cs + 16),  lim = s while the record has not started, else e - 1,
-// so segment j of round rr is interior iff rel >= 16 (8 rr + j) -- one v_cmp
-// against an immediate, then the wave vote.  rel changes only in the slow path.
-template <bool FRAME>
-__global__ __launch_bounds__(kVerify2Threads) void k_verify_records4(const uint8_t* __restrict__ image, uint64_t nbytes,
-                                                                     uint64_t base_offset,
-                                                                     const uint32_t* __restrict__ first,
-                                                                     revel_record_result* __restrict__ out,
-                                                                     uint32_t lead,
-                                                                     const uint64_t* __restrict__ hlist,
-                                                                     const uint32_t* __restrict__ counts) {
-    __shared__ uint32_t tab[32768];
-    __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
-    fill_tables<TM_S4R>(tab);
-    __syncthreads();
-    VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
-    const LaneConst L = make_lane_const();
-    const uint32_t lane = lane_id();
-    const uint64_t vbytes = nbytes + lead;
-    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;  // whole blocks [b_lo, b_hi)
-    const uint64_t waves_per_wg = kVerify2Threads / 64;
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-    constexpr uint32_t kNone = 0xFFFFFFFFu;
-    const bool use_list = hlist != nullptr && counts != nullptr;
-    const uint32_t cs = lane * 512u, ce = cs + 512u;
-
-    // wave-uniform block index (readfirstlane: the compiler cannot prove that
-    // threadIdx.x >> 6 is uniform, and would keep the block arithmetic in VGPRs)
-    const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint64_t b = b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
-    if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
-    uint4 cur[8], nxt[8];
-    uint32_t pf_count = kNone, pf_first = 0;
-    uint64_t pf_hl = 0;
-    auto load_round = [&](const uint8_t* blk, uint4* v, int rr) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + rr * 128 + j * 16));
-    };
-    // header list first: the list is needed before the data (loads return in order)
-    auto prefetch = [&](uint64_t nb) {
-        if (use_list) {
-            pf_count = counts[nb];
-            pf_hl = hlist[nb * kListPerBlock + lane];
-        }
-        if constexpr (!FRAME) pf_first = first[nb];
-        load_round(image + nb * kBlockSize - lead, cur, 0);
-    };
-    prefetch(b);
-    while (b < b_hi) {
-        const uint64_t base = b * kBlockSize;
-        const uint8_t* blk = image + base - lead;
-        const uint64_t bn = b + nwaves;
-        const uint32_t nlist = pf_count;
-        const uint64_t hl_e = pf_hl;
-        uint32_t out_base = pf_first;
-        uint32_t walk_from = 0;
-        bool have_round0 = true;
-        for (;;) {
-            const bool from_list = walk_from == 0 && nlist <= kListPerBlock;
-            if (from_list) {
-                // headers come from the count pass; offsets by prefix sum; the
-                // finalizer reads them back from LDS (no global header reads)
-                const Hdr h = list_header(hl_e);
-                const uint32_t off = wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
-                if (lane < nlist) {
-                    const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
-                    wl.off[lane] = (uint16_t)off;
-                    wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
-                    wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
-                    wl.acc[lane] = 0;
-                    wl.hstored[lane] = h.stored;
-                    wl.hlt[lane] = h.len | (h.type << 16);
-                }
-                if (lane == 0) {
-                    wl.s[nlist] = wl.em1[nlist] = kNoRange;
-                    wl.nrec = nlist;
-                    wl.more_off = kNone;
-                }
-            } else if (lane == 0) {
-                uint32_t off = walk_from, n = 0, cont = kNone;
-                while (kBlockSize - off >= kHeaderSize) {
-                    if (n == kRecCap2) { cont = off; break; }
-                    const Hdr h = read_header(blk, off, kBlockSize);
-                    const uint32_t st = classify(h, off, kBlockSize);
-                    const bool bad = st != REVEL_REC_OK;
-                    wl.off[n] = (uint16_t)off;
-                    wl.s[n] = bad ? kNoRange : (uint16_t)(off + 6);
-                    wl.em1[n] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
-                    wl.acc[n] = 0;
-                    ++n;
-                    if (bad) break;
-                    off += kHeaderSize + h.len;
-                }
-                wl.s[n] = wl.em1[n] = kNoRange;
-                wl.nrec = n;
-                wl.more_off = cont;
-            }
-            wave_lds_sync();
-            const uint32_t nrec = wl.nrec;
-            const uint32_t cont = wl.more_off;
-            auto load_rec = [&](uint32_t k, uint32_t& s, uint32_t& e) {
-                s = wl.s[k];  // k <= nrec: the sentinel ends every list
-                e = uint32_t(wl.em1[k]) + 1u;
-            };
-            uint32_t lo = 0, hi = nrec;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
-            }
-            uint32_t r = lo, s, e;
-            load_rec(r, s, e);
-            const bool active = r < nrec && s < ce;
-            uint32_t state = 0;
-            int32_t rel = int32_t(s >= cs ? s : e - 1u) - int32_t(cs + 16u);
-            if (__any(active)) {
-                if (!have_round0) load_round(blk, cur, 0);
 #pragma unroll 1
                 for (int rr = 0; rr < 4; ++rr) {
                     if (rr < 3) load_round(blk, nxt, rr + 1);
@@ -1368,7 +1149,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records4(const uint8
                     for (int j = 0; j < 8; ++j) {
                         const uint32_t p16 = cs + rr * 128 + j * 16;
                         // don't-care gap before the next record, or strictly inside one
-                        if (__all(rel >= rr * 128 + j * 16)) {
+                        const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
+                        if (__all(interior)) {
                             state = absorb4<TM_S4R>(state, cur[j], L, tab);
                         } else {
                             const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
@@ -1400,8 +1182,6 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records4(const uint8
                                     load_rec(r, s, e);
                                 }
                             }
-                            const uint32_t pn = p16 + 16u;  // the next segment
-                            rel = int32_t(s >= pn ? s : e - 1u) - int32_t(cs + 16u);
                         }
                     }
                     __builtin_amdgcn_sched_barrier(0);
@@ -2103,27 +1883,12 @@ static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
 
 // Whole blocks on `grid` workgroups, then (only if there is one) the partial
 // first/last block on one more workgroup, same stream.
-template <bool FRAME>
-static hipError_t launch_verify4(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
-                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
-    hipLaunchKernelGGL((k_verify_records4<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
-                       base_offset, d_first, d_out, lead, hl, d_counts);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !partial) return e;
-    // <= 2 partial blocks: one single-wave workgroup each, 4 KiB unreplicated tables
-    // (a 128 KiB table fill and one latency-bound wave cost ~50 us per launch)
-    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64>), dim3(2), dim3(64), 0, st, img,
-                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
-    return hipGetLastError();
-}
-
 // Production: pipelined whole-block kernel + the partial blocks on one workgroup.
-template <bool FRAME, int DIAG = 0>
+template <bool FRAME>
 static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                  uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
-    hipLaunchKernelGGL((k_verify_records3<FRAME, DIAG>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
+    hipLaunchKernelGGL((k_verify_records3<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !partial) return e;
@@ -2175,20 +1940,12 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts);
             return hipGetLastError();
-        case 8: return launch_verify4<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                             d_counts, st);
-        case 21: return launch_verify3<false, 1>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                 d_counts, st);
-        case 22: return launch_verify3<false, 2>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                 d_counts, st);
-        case 23: return launch_verify3<false, 4>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                 d_counts, st);
-        case 24: return launch_verify3<false, 6>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                 d_counts, st);
         case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
                                                        hl, d_counts, st);
-        default: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                              d_counts, st);
+        case 0:
+        case 2: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                             d_counts, st);
+        default: return hipErrorInvalidValue;
     }
 }
 

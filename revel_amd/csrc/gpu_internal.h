@@ -49,8 +49,12 @@ hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, u
 hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
                         const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
                         hipStream_t st);
-// variant 0 = production (uses the header list when given), 1 = round-1 kernel,
-// 2 = production kernel forced to walk headers itself.
+// C3 verify variants: 0 = production (k_verify_records3 whole blocks + a
+// single-wave launch for partial blocks; header list when given), 1 = round-1
+// kernel (v1), 2 = production forced to walk headers itself, 3 / 4 = v2 with
+// the masked boundary path (with / without the wave vote), 5 = v2 as one
+// kernel for whole and partial blocks, 6 = v2 split into whole/partial launches.
+// Other values: hipErrorInvalidValue.
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                   const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st);
