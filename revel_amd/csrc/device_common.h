@@ -1,0 +1,385 @@
+// device_common.h -- device helpers shared by the gfx950 kernel files
+// (k_blocks.hip, k_records.hip, k_reasm.hip).  Everything here has internal
+// linkage (anonymous namespace): each translation unit gets its own copy of
+// the constant tables, so no relocatable device code is needed.
+//
+// The CRC-32C engine for Revel's WAL record path (CDNA4 / gfx950).
+//
+// Hot path (reference guimingyue/revel @ v0):
+//   log_writer.rs:107-111  crc = mask(extend(type, payload))  (writer side)
+//   log_reader.rs:200-206  unmask(stored) == value(type||payload) (reader side)
+//   util/crc.rs:13-44      CRC_32_ISCSI + mask/unmask
+//
+// Work decomposition: ONE WAVEFRONT PER 32 KiB LOG BLOCK.  Lane i owns the
+// contiguous 512-byte chunk [512 i, 512 i + 512) of its block and runs a
+// table-driven CRC over it from a zero register; the 64 partial registers are
+// then combined by a wavefront GF(2) polynomial-shift reduction:
+//     R(block) = XOR_i  R_i * x^(8*512*(63-i))  mod P
+// (each lane multiplies by its own constant, then an xor-butterfly across the
+// wave).  Init/xorout enter once per record as a length-dependent constant.
+// No MFMA: this is GF(2) arithmetic, not a contraction.
+//
+// Lookup tables live in LDS, replicated 32x so that lane (l & 31) always hits
+// bank (l & 31) for ds_read_b32: bank-conflict-free gathers whatever the data.
+// The LDS byte address of entry e for lane l is (e << 8) | ((l & 31) << 2)
+// | (region << 16), built by ONE v_perm_b32 per lookup.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "crc32c_math.h"
+#include "gpu_internal.h"
+
+namespace {
+using namespace revel;
+
+constexpr SliceTables kTables = make_slice_tables();
+
+// ---------------------------------------------------------------------------
+// Compile-time GF(2) constants
+// ---------------------------------------------------------------------------
+struct LaneShiftConsts {
+    uint32_t c[64];  // x^(8*512*(63-i)) mod P
+};
+constexpr LaneShiftConsts make_lane_shift() {
+    LaneShiftConsts s{};
+    for (int i = 0; i < 64; ++i) s.c[i] = x8n(512ull * (63 - i));
+    return s;
+}
+// x^(8*512*m) for m = 0..64 and x^(8*d) for d = 0..512: any shift inside a
+// block is one multmodp of two table entries.
+struct ShiftTables {
+    uint32_t chunk[65];
+    uint32_t byte[513];
+};
+constexpr ShiftTables make_shift_tables() {
+    ShiftTables s{};
+    for (int m = 0; m <= 64; ++m) s.chunk[m] = x8n(512ull * m);
+    uint32_t v = 0x80000000u;  // x^0
+    const uint32_t x8 = x8n(1);
+    for (int d = 0; d <= 512; ++d) {
+        s.byte[d] = v;
+        v = multmodp(x8, v);
+    }
+    return s;
+}
+
+__constant__ SliceTables c_tables = kTables;
+__constant__ LaneShiftConsts c_lane_shift = make_lane_shift();
+__constant__ ShiftTables c_shift = make_shift_tables();
+
+constexpr uint32_t kFullInitXor = init_xor(kFullCrcLen);
+constexpr uint32_t kFullTypeByte = 1u;
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Branch-free a*b mod P (reflected).  v_bfe_i32 turns a bit into 0/-1.
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        uint32_t am = (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - k, 1);
+        p ^= b & am;
+        uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
+        b = (b >> 1) ^ (kPolyReflected & bm);
+    }
+    return p;
+}
+
+// x^(8n) mod P for 0 <= n <= 32768 from the two shift tables.
+__device__ __forceinline__ uint32_t gf_x8n_block(uint32_t n) {
+    uint32_t m = n >> 9, d = n & 511u;
+    uint32_t a = c_shift.chunk[m];
+    return d ? gf_mul(a, c_shift.byte[d]) : a;
+}
+
+__device__ __forceinline__ uint32_t xor_reduce_wave(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t bytewise_step(uint32_t s, uint32_t b) {
+    return c_tables.t[0][(s ^ b) & 0xffu] ^ (s >> 8);
+}
+
+// LDS byte-address load (ds_read_b32 with immediate offset).  The tables are
+// a static __shared__ array, so its base folds into the instruction.
+template <int OFF>
+__device__ __forceinline__ uint32_t ldsw(const uint32_t* tab, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr + OFF);
+}
+
+// v_perm_b32 selectors: result byte0 <- lanec byte0 (lane*4), byte1 <- x byte k,
+// byte2 <- lanec byte2 (table region), byte3 <- 0.
+template <int K>
+struct Sel {
+    static constexpr uint32_t v = 0x0C020000u | ((4u + K) << 8) | 0x00u;
+};
+
+// ---------------------------------------------------------------------------
+// Table modes
+// ---------------------------------------------------------------------------
+enum TableMode : int {
+    TM_S4R = 0,  // slice-by-4, 32x replicated, 128 KiB LDS
+    TM_S2R = 1,  // slice-by-2, 32x replicated, 64 KiB LDS
+    TM_S4 = 2,   // slice-by-4, unreplicated, 4 KiB LDS (bank conflicts)
+};
+
+template <int TM>
+struct TableCfg;
+template <>
+struct TableCfg<TM_S4R> {
+    static constexpr uint32_t bytes = 131072;
+};
+template <>
+struct TableCfg<TM_S2R> {
+    static constexpr uint32_t bytes = 65536;
+};
+template <>
+struct TableCfg<TM_S4> {
+    static constexpr uint32_t bytes = 4096;
+};
+
+// Fill the LDS image of the tables (cooperatively, whole workgroup).
+template <int TM>
+__device__ void fill_tables(uint32_t* tab) {
+    const uint32_t ndw = TableCfg<TM>::bytes / 4;
+    for (uint32_t d = threadIdx.x; d < ndw; d += blockDim.x) {
+        uint32_t v;
+        if constexpr (TM == TM_S4) {
+            // [T3 | T2 | T1 | T0], 256 entries each: byte k of x indexes T(3-k)
+            v = c_tables.t[3 - (d >> 8)][d & 255u];
+        } else if constexpr (TM == TM_S4R) {
+            // region r (16384 dw) -> row e (64 dw) -> half h (32 dw) -> copy c
+            uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
+            // byte0 -> T3 (r0 h0), byte1 -> T2 (r0 h1), byte2 -> T1 (r1 h0), byte3 -> T0 (r1 h1)
+            v = c_tables.t[3 - (r * 2 + h)][e];
+        } else {
+            // S2R: row e = [T1 x32 | T0 x32]
+            uint32_t e = (d >> 6) & 255u, h = (d >> 5) & 1u;
+            v = c_tables.t[1 - h][e];
+        }
+        tab[d] = v;
+    }
+}
+
+struct LaneConst {
+    uint32_t lc0, lc1;
+};
+
+__device__ __forceinline__ LaneConst make_lane_const() {
+    uint32_t c4 = (lane_id() & 31u) << 2;
+    return {c4, c4 | 0x10000u};
+}
+
+// Absorb one little-endian 32-bit word into the raw register.
+template <int TM>
+__device__ __forceinline__ uint32_t absorb(uint32_t crc, uint32_t w, LaneConst L, const uint32_t* tab) {
+    uint32_t x = crc ^ w;
+    if constexpr (TM == TM_S4R) {
+        uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
+        uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
+        uint32_t a2 = __builtin_amdgcn_perm(x, L.lc1, Sel<2>::v);
+        uint32_t a3 = __builtin_amdgcn_perm(x, L.lc1, Sel<3>::v);
+        return (ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1)) ^ (ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3));
+    } else if constexpr (TM == TM_S2R) {
+        uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
+        uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
+        uint32_t c = ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1) ^ (x >> 16);
+        uint32_t a2 = __builtin_amdgcn_perm(c, L.lc0, Sel<0>::v);
+        uint32_t a3 = __builtin_amdgcn_perm(c, L.lc0, Sel<1>::v);
+        return ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3) ^ (c >> 16);
+    } else {
+        return (tab[x & 0xffu] ^ tab[256 + ((x >> 8) & 0xffu)]) ^
+               (tab[512 + ((x >> 16) & 0xffu)] ^ tab[768 + (x >> 24)]);
+    }
+}
+
+template <int TM>
+__device__ __forceinline__ uint32_t absorb4(uint32_t crc, uint4 v, LaneConst L, const uint32_t* tab) {
+    crc = absorb<TM>(crc, v.x, L, tab);
+    crc = absorb<TM>(crc, v.y, L, tab);
+    crc = absorb<TM>(crc, v.z, L, tab);
+    crc = absorb<TM>(crc, v.w, L, tab);
+    return crc;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldg4(const uint4* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ldg4_plain(const uint4* p) { return *p; }
+
+// How a lane's 512-byte chunk reaches registers.
+enum LoadMode : int {
+    LM_DIRECT_NT = 0,     // lane loads its own chunk, nontemporal (64 lines per instruction)
+    LM_DIRECT = 1,        // same, default cache policy
+    LM_STAGED = 2,        // line-coalesced loads (8 whole lines per instruction) + LDS transpose
+};
+
+// Staging layout (one 8 KiB buffer per wave per round): piece t (16 B) of
+// owner lane i sits in slot t*64 + (i ^ t).  ds_write_b128 by the loading
+// lanes and ds_read_b128 by the owners are both bank-conflict-free.
+__device__ __forceinline__ uint32_t stage_slot(uint32_t owner, uint32_t t) { return t * 64u + (owner ^ t); }
+
+// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
+// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
+// Returns lane 0's first 16 bytes through *hdr.
+__device__ __forceinline__ void zero_header_bytes(uint4& v, bool l0, bool force_type, uint4* hdr) {
+    *hdr = v;
+    v.x = l0 ? 0u : v.x;
+    const uint32_t y = force_type ? ((v.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16)) : v.y;
+    v.y = l0 ? (y & 0xFFFF0000u) : v.y;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
+// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
+// Returns lane 0's first 16 bytes through *hdr.
+template <int TM, int LM>
+__device__ __forceinline__ uint32_t full_block_lane_crc(const uint8_t* blk, LaneConst L, const uint32_t* tab,
+                                                        uint4* stage, uint4* hdr, bool force_type) {
+    const uint32_t lane = lane_id();
+    const bool l0 = lane == 0;
+    uint32_t crc = 0;
+    uint4 cur[8], nxt[8];
+    // Round r covers bytes [512 i + 128 r, +128) of every lane i.
+    auto load_round = [&](uint4* v, int r) {
+        if constexpr (LM == LM_STAGED) {
+            // instruction k: lanes 8m..8m+7 read the whole 128-B line of owner 8k+m
+            const uint8_t* base = blk + (lane >> 3) * 512u + r * 128 + (lane & 7u) * 16u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = ldg4(reinterpret_cast<const uint4*>(base + k * 8 * 512));
+        } else {
+            const uint4* p = reinterpret_cast<const uint4*>(blk + lane * 512u + r * 128);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = LM == LM_DIRECT_NT ? ldg4(p + j) : ldg4_plain(p + j);
+        }
+    };
+    load_round(cur, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (r < 3) load_round(nxt, r + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (LM == LM_STAGED) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) stage[stage_slot(8u * k + (lane >> 3), lane & 7u)] = cur[k];
+            wave_lds_sync();
+#pragma unroll
+            for (int t = 0; t < 8; ++t) cur[t] = stage[stage_slot(lane, t)];
+            wave_lds_sync();
+        }
+        if (r == 0) zero_header_bytes(cur[0], l0, force_type, hdr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) crc = absorb4<TM>(crc, cur[j], L, tab);
+        __builtin_amdgcn_sched_barrier(0);
+        if (r < 3) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+        }
+    }
+    return crc;
+}
+
+// ---------------------------------------------------------------------------
+// Config C3: variable records (FULL/FIRST/MIDDLE/LAST mixes, padding, zeros).
+// ---------------------------------------------------------------------------
+struct Hdr {
+    uint32_t stored, len, type;
+};
+
+// Bytes [off, off+7) of a block of length bl, never reading at or past bl
+// (the image end need not be 4-byte aligned or padded).
+__device__ __forceinline__ Hdr read_header(const uint8_t* base, uint32_t off, uint32_t bl) {
+    const uint32_t a0 = off & ~3u;
+    uint32_t w0, w1, w2 = 0;
+    if (a0 + 12u <= bl) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(base + a0);
+        w0 = w[0]; w1 = w[1]; w2 = w[2];
+    } else {
+        uint8_t t[12];
+        for (uint32_t k = 0; k < 12; ++k) t[k] = a0 + k < bl ? base[a0 + k] : 0;
+        memcpy(&w0, t, 4); memcpy(&w1, t + 4, 4); memcpy(&w2, t + 8, 4);
+    }
+    const uint32_t sh = (off & 3u) * 8u;
+    const uint64_t lo = (uint64_t(w1) << 32) | w0;
+    const uint64_t hi = (uint64_t(w2) << 32) | w1;
+    const uint32_t a = uint32_t(lo >> sh);  // bytes off..off+3
+    const uint32_t b = uint32_t(hi >> sh);  // bytes off+4..off+7
+    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
+}
+
+// 16 bytes at block offset pos, zero outside [lo, bl) (lo > 0 only for the
+// first block of an image that starts mid-block).
+__device__ __forceinline__ uint4 load16_range(const uint8_t* blk, uint32_t pos, uint32_t lo, uint32_t bl) {
+    if (pos >= lo && pos + 16u <= bl) return ldg4_plain(reinterpret_cast<const uint4*>(blk + pos));
+    uint8_t t[16];
+    for (uint32_t k = 0; k < 16; ++k) t[k] = (pos + k >= lo && pos + k < bl) ? blk[pos + k] : 0;
+    uint4 v;
+    memcpy(&v, t, 16);
+    return v;
+}
+
+__device__ __forceinline__ Hdr read_header_range(const uint8_t* base, uint32_t off, uint32_t lo, uint32_t bl) {
+    if ((off & ~3u) >= lo) return read_header(base, off, bl);
+    uint8_t t[8];
+    for (uint32_t k = 0; k < 7; ++k) t[k] = base[off + k];  // off >= lo, off + 7 <= bl
+    t[7] = 0;
+    uint32_t a, b;
+    memcpy(&a, t, 4);
+    memcpy(&b, t + 4, 4);
+    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
+}
+
+// 16 bytes at block offset pos, zero past bl.
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* blk, uint32_t pos, uint32_t bl) {
+    if (pos + 16u <= bl) return ldg4(reinterpret_cast<const uint4*>(blk + pos));
+    uint8_t t[16];
+    for (uint32_t k = 0; k < 16; ++k) t[k] = pos + k < bl ? blk[pos + k] : 0;
+    uint4 v;
+    memcpy(&v, t, 16);
+    return v;
+}
+
+// One step of the physical-record walk (oracle walk_block rules).
+__device__ __forceinline__ uint32_t classify(const Hdr& h, uint32_t off, uint32_t bl) {
+    if (kHeaderSize + h.len > bl - off) return REVEL_REC_BAD_LENGTH;
+    if (h.type == 0 && h.len == 0) return REVEL_REC_ZERO;
+    return REVEL_REC_OK;
+}
+
+// Header-list entry: the 7 header bytes as read (stored CRC | len << 32 |
+// type << 48).  Offsets are not stored: entry k sits at the sum of 7 + len of
+// the entries before it (a wave prefix sum in the consumer).
+__device__ __forceinline__ uint64_t list_entry(const Hdr& h) {
+    return uint64_t(h.stored) | (uint64_t(h.len | (h.type << 16)) << 32);
+}
+__device__ __forceinline__ Hdr list_header(uint64_t e) {
+    const uint32_t hi = uint32_t(e >> 32);
+    return {uint32_t(e), hi & 0xFFFFu, (hi >> 16) & 0xFFu};
+}
+// Wave-wide exclusive prefix sum (lanes >= n contribute 0).
+__device__ __forceinline__ uint32_t wave_exclusive_sum(uint32_t v) {
+    uint32_t incl = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        incl += lane_id() >= d ? t : 0u;
+    }
+    return incl - v;
+}
+
+}  // namespace

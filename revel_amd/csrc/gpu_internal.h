@@ -1,5 +1,6 @@
 // gpu_internal.h -- internal interface between the C-ABI layer and the
-// gfx950 kernels in gpu_crc.hip.  Not installed; see include/revel_wal.h.
+// gfx950 kernels (k_blocks.hip, k_records.hip, k_reasm.hip, batch.hip).  Not
+// installed; see include/revel_wal.h.
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -24,7 +25,7 @@ struct DeviceInfo {
 };
 
 // variant: 0 = production (S2R, 512 threads, 2 WG/CU); others are the
-// experiment arms listed in gpu_crc.hip (100 = streaming-read ceiling).
+// experiment arms listed in k_blocks.hip (100 = streaming-read ceiling).
 hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void* d_blocks, uint64_t n,
                                    uint32_t* d_masked, uint8_t* d_ok, hipStream_t st);
 hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st);

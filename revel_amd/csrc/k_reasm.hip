@@ -1,0 +1,174 @@
+// k_reasm.hip -- device replay reassembly (log_reader.rs:76-153, LevelDB-correct):
+// classify / emit / gather of logical records from the physical-record array.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "device_common.h"
+
+using namespace revel;
+
+namespace {
+// ---------------------------------------------------------------------------
+// Device replay reassembly (log_reader.rs:76-153, LevelDB-correct; the rules
+// of oracle LogReader / replay_events): physical records -> events in file
+// order: RECORD (FULL, or FIRST MIDDLE* LAST all valid) or ERROR (zero record,
+// length past the block that is not the torn tail of the image, checksum
+// mismatch when checking, unknown type).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool reasm_is_error(const revel_record_result& r, bool checksum, bool tail) {
+    if (r.status == REVEL_REC_ZERO) return true;
+    if (r.status == REVEL_REC_BAD_LENGTH) return !tail;
+    if (checksum && r.status == REVEL_REC_BAD_CHECKSUM) return true;
+    return r.type < REVEL_FULL_TYPE || r.type > REVEL_LAST_TYPE;
+}
+
+__global__ void k_reasm_classify(const revel_record_result* __restrict__ phys, uint64_t n, uint64_t image_end,
+                                 int checksum, uint32_t* __restrict__ ev_flag, uint64_t* __restrict__ ev_len,
+                                 uint32_t* __restrict__ ev_end) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const revel_record_result r = phys[i];
+        auto tail_of = [&](uint64_t k, const revel_record_result& q) {
+            return k == n - 1 && q.status == REVEL_REC_BAD_LENGTH && q.file_offset + kHeaderSize + q.length > image_end;
+        };
+        uint32_t flag = 0, end = (uint32_t)i;
+        uint64_t len = 0;
+        const bool tail = tail_of(i, r);
+        if (reasm_is_error(r, checksum, tail)) {
+            flag = 1;  // ERROR event
+        } else if (!tail) {
+            if (r.type == REVEL_FULL_TYPE) {
+                flag = 1;
+                len = r.length;
+            } else if (r.type == REVEL_FIRST_TYPE) {
+                uint64_t acc = r.length;
+                for (uint64_t j = i + 1; j < n; ++j) {
+                    const revel_record_result q = phys[j];
+                    if (reasm_is_error(q, checksum, tail_of(j, q)) || tail_of(j, q)) break;
+                    if (q.type == REVEL_MIDDLE_TYPE) {
+                        acc += q.length;
+                        continue;
+                    }
+                    if (q.type == REVEL_LAST_TYPE) {
+                        flag = 1;
+                        len = acc + q.length;
+                        end = (uint32_t)j;
+                    }
+                    break;  // FULL / FIRST: this fragment is dropped
+                }
+            }
+        }
+        ev_flag[i] = flag;
+        ev_len[i] = len;
+        ev_end[i] = end;
+    }
+}
+
+__global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint64_t n, uint64_t image_end, int checksum,
+                             const uint32_t* __restrict__ ev_flag, const uint32_t* __restrict__ ev_idx,
+                             const uint64_t* __restrict__ pay_off, const uint32_t* __restrict__ ev_end,
+                             revel_logical_record* __restrict__ out, uint64_t* __restrict__ frag_dst) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!ev_flag[i]) continue;
+        const revel_record_result r = phys[i];
+        const bool tail = i == n - 1 && r.status == REVEL_REC_BAD_LENGTH &&
+                          r.file_offset + kHeaderSize + r.length > image_end;
+        revel_logical_record o;
+        o.file_offset = r.file_offset;
+        o.payload_offset = pay_off[i];
+        o.first_phys = (uint32_t)i;
+        o.last_phys = ev_end[i];
+        o.reserved[0] = o.reserved[1] = o.reserved[2] = 0;
+        if (reasm_is_error(r, checksum, tail)) {
+            o.length = 0;
+            o.status = r.status == REVEL_REC_OK || (!checksum && r.status == REVEL_REC_BAD_CHECKSUM)
+                           ? REVEL_LOGICAL_BAD_TYPE
+                           : r.status;
+        } else {
+            uint64_t acc = 0;
+            for (uint64_t k = i; k <= ev_end[i]; ++k) {
+                frag_dst[k] = pay_off[i] + acc;
+                acc += phys[k].length;
+            }
+            o.length = (uint32_t)acc;
+            o.status = REVEL_LOGICAL_OK;
+        }
+        out[ev_idx[i]] = o;
+    }
+}
+
+// One wave copies len bytes src -> dst, any byte alignment of either: a byte
+// head up to dst's next 16-B boundary, then aligned 16-B stores whose source
+// bytes are funnel-shifted (v_alignbyte) out of 4-B-aligned dword loads (never
+// reading past the source range), then a byte tail.  Coalesced both ways.
+__device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
+    const uint32_t lane = lane_id();
+    const uint32_t head = min(len, (16u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
+    if (lane < head) dst[lane] = src[lane];
+    const uint8_t* s = src + head;
+    uint8_t* d = dst + head;
+    const uint32_t n = len - head;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s - sh);
+    // vector v reads s4[4v .. 4v+3] (+ s4[4v+4] when sh != 0): stay inside [s, s+n)
+    const uint32_t nvec = sh == 0 ? n / 16u : (n + sh >= 20u ? (n + sh - 20u) / 16u + 1u : 0u);
+    for (uint32_t v = lane; v < nvec; v += 64) {
+        const uint32_t* q = s4 + 4u * v;
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = sh ? q[4] : 0u;
+        uint4 o;
+        o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        *reinterpret_cast<uint4*>(d + 16u * v) = o;
+    }
+    for (uint32_t i = nvec * 16u + lane; i < n; i += 64) d[i] = s[i];
+}
+
+// One wave per physical record that belongs to an emitted logical record.
+__global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image_base,
+                               const revel_record_result* __restrict__ phys, uint64_t n,
+                               const uint64_t* __restrict__ frag_dst, uint8_t* __restrict__ payload) {
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t k = w0; k < n; k += waves) {
+        const uint64_t dst = frag_dst[k];
+        if (dst == ~0ull) continue;
+        const revel_record_result r = phys[k];
+        wave_copy(image + (r.file_offset - image_base) + kHeaderSize, payload + dst, r.length);
+    }
+}
+
+}  // namespace
+
+namespace revel {
+hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
+                          int checksum, uint32_t* d_flag, uint64_t* d_len, uint32_t* d_end, hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));
+    hipLaunchKernelGGL(k_reasm_classify, dim3((uint32_t)grid), dim3(256), 0, st, d_phys, n, image_end, checksum, d_flag,
+                       d_len, d_end);
+    return hipGetLastError();
+}
+
+hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
+                      int checksum, const uint32_t* d_flag, const uint32_t* d_idx, const uint64_t* d_off,
+                      const uint32_t* d_end, revel_logical_record* d_out, uint64_t* d_frag_dst, hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));
+    hipLaunchKernelGGL(k_reasm_emit, dim3((uint32_t)grid), dim3(256), 0, st, d_phys, n, image_end, checksum, d_flag,
+                       d_idx, d_off, d_end, d_out, d_frag_dst);
+    return hipGetLastError();
+}
+
+hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
+                        const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
+                        hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 3) / 4));
+    hipLaunchKernelGGL(k_reasm_gather, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<const uint8_t*>(d_image),
+                       image_base, d_phys, n, d_frag_dst, static_cast<uint8_t*>(d_payload));
+    return hipGetLastError();
+}
+
+}  // namespace revel

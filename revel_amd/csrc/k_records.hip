@@ -1,465 +1,18 @@
-// gpu_crc.hip -- CDNA4 (gfx950) CRC-32C engine for Revel's WAL record path.
-//
-// Hot path (reference guimingyue/revel @ v0):
-//   log_writer.rs:107-111  crc = mask(extend(type, payload))  (writer side)
-//   log_reader.rs:200-206  unmask(stored) == value(type||payload) (reader side)
-//   util/crc.rs:13-44      CRC_32_ISCSI + mask/unmask
-//
-// Work decomposition: ONE WAVEFRONT PER 32 KiB LOG BLOCK.  Lane i owns the
-// contiguous 512-byte chunk [512 i, 512 i + 512) of its block and runs a
-// table-driven CRC over it from a zero register; the 64 partial registers are
-// then combined by a wavefront GF(2) polynomial-shift reduction:
-//     R(block) = XOR_i  R_i * x^(8*512*(63-i))  mod P
-// (each lane multiplies by its own constant, then an xor-butterfly across the
-// wave).  Init/xorout enter once per record as a length-dependent constant.
-// No MFMA: this is GF(2) arithmetic, not a contraction.
-//
-// Lookup tables live in LDS, replicated 32x so that lane (l & 31) always hits
-// bank (l & 31) for ds_read_b32: bank-conflict-free gathers whatever the data.
-// The LDS byte address of entry e for lane l is (e << 8) | ((l & 31) << 2)
-// | (region << 16), built by ONE v_perm_b32 per lookup.
+// k_records.hip -- config C3 kernels: per-block header walk (count + header
+// list), exclusive scans, record verify (production k_verify_records3 and the
+// experiment arms), device append framing and the replay summaries.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
 #include <type_traits>
-#include <string>
-#include <vector>
 
-#include "crc32c_math.h"
-#include "gpu_internal.h"
+#include "device_common.h"
 
 using namespace revel;
 
 namespace {
-
-constexpr SliceTables kTables = make_slice_tables();
-
-// ---------------------------------------------------------------------------
-// Compile-time GF(2) constants
-// ---------------------------------------------------------------------------
-struct LaneShiftConsts {
-    uint32_t c[64];  // x^(8*512*(63-i)) mod P
-};
-constexpr LaneShiftConsts make_lane_shift() {
-    LaneShiftConsts s{};
-    for (int i = 0; i < 64; ++i) s.c[i] = x8n(512ull * (63 - i));
-    return s;
-}
-// x^(8*512*m) for m = 0..64 and x^(8*d) for d = 0..512: any shift inside a
-// block is one multmodp of two table entries.
-struct ShiftTables {
-    uint32_t chunk[65];
-    uint32_t byte[513];
-};
-constexpr ShiftTables make_shift_tables() {
-    ShiftTables s{};
-    for (int m = 0; m <= 64; ++m) s.chunk[m] = x8n(512ull * m);
-    uint32_t v = 0x80000000u;  // x^0
-    const uint32_t x8 = x8n(1);
-    for (int d = 0; d <= 512; ++d) {
-        s.byte[d] = v;
-        v = multmodp(x8, v);
-    }
-    return s;
-}
-
-__constant__ SliceTables c_tables = kTables;
-__constant__ LaneShiftConsts c_lane_shift = make_lane_shift();
-__constant__ ShiftTables c_shift = make_shift_tables();
-
-constexpr uint32_t kFullInitXor = init_xor(kFullCrcLen);
-constexpr uint32_t kFullTypeByte = 1u;
-
-// ---------------------------------------------------------------------------
-// Device helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-
-// Branch-free a*b mod P (reflected).  v_bfe_i32 turns a bit into 0/-1.
-__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
-    uint32_t p = 0;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        uint32_t am = (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - k, 1);
-        p ^= b & am;
-        uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
-        b = (b >> 1) ^ (kPolyReflected & bm);
-    }
-    return p;
-}
-
-// x^(8n) mod P for 0 <= n <= 32768 from the two shift tables.
-__device__ __forceinline__ uint32_t gf_x8n_block(uint32_t n) {
-    uint32_t m = n >> 9, d = n & 511u;
-    uint32_t a = c_shift.chunk[m];
-    return d ? gf_mul(a, c_shift.byte[d]) : a;
-}
-
-__device__ __forceinline__ uint32_t xor_reduce_wave(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t bytewise_step(uint32_t s, uint32_t b) {
-    return c_tables.t[0][(s ^ b) & 0xffu] ^ (s >> 8);
-}
-
-// LDS byte-address load (ds_read_b32 with immediate offset).  The tables are
-// a static __shared__ array, so its base folds into the instruction.
-template <int OFF>
-__device__ __forceinline__ uint32_t ldsw(const uint32_t* tab, uint32_t byte_addr) {
-    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr + OFF);
-}
-
-// v_perm_b32 selectors: result byte0 <- lanec byte0 (lane*4), byte1 <- x byte k,
-// byte2 <- lanec byte2 (table region), byte3 <- 0.
-template <int K>
-struct Sel {
-    static constexpr uint32_t v = 0x0C020000u | ((4u + K) << 8) | 0x00u;
-};
-
-// ---------------------------------------------------------------------------
-// Table modes
-// ---------------------------------------------------------------------------
-enum TableMode : int {
-    TM_S4R = 0,  // slice-by-4, 32x replicated, 128 KiB LDS
-    TM_S2R = 1,  // slice-by-2, 32x replicated, 64 KiB LDS
-    TM_S4 = 2,   // slice-by-4, unreplicated, 4 KiB LDS (bank conflicts)
-};
-
-template <int TM>
-struct TableCfg;
-template <>
-struct TableCfg<TM_S4R> {
-    static constexpr uint32_t bytes = 131072;
-};
-template <>
-struct TableCfg<TM_S2R> {
-    static constexpr uint32_t bytes = 65536;
-};
-template <>
-struct TableCfg<TM_S4> {
-    static constexpr uint32_t bytes = 4096;
-};
-
-// Fill the LDS image of the tables (cooperatively, whole workgroup).
-template <int TM>
-__device__ void fill_tables(uint32_t* tab) {
-    const uint32_t ndw = TableCfg<TM>::bytes / 4;
-    for (uint32_t d = threadIdx.x; d < ndw; d += blockDim.x) {
-        uint32_t v;
-        if constexpr (TM == TM_S4) {
-            // [T3 | T2 | T1 | T0], 256 entries each: byte k of x indexes T(3-k)
-            v = c_tables.t[3 - (d >> 8)][d & 255u];
-        } else if constexpr (TM == TM_S4R) {
-            // region r (16384 dw) -> row e (64 dw) -> half h (32 dw) -> copy c
-            uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
-            // byte0 -> T3 (r0 h0), byte1 -> T2 (r0 h1), byte2 -> T1 (r1 h0), byte3 -> T0 (r1 h1)
-            v = c_tables.t[3 - (r * 2 + h)][e];
-        } else {
-            // S2R: row e = [T1 x32 | T0 x32]
-            uint32_t e = (d >> 6) & 255u, h = (d >> 5) & 1u;
-            v = c_tables.t[1 - h][e];
-        }
-        tab[d] = v;
-    }
-}
-
-struct LaneConst {
-    uint32_t lc0, lc1;
-};
-
-__device__ __forceinline__ LaneConst make_lane_const() {
-    uint32_t c4 = (lane_id() & 31u) << 2;
-    return {c4, c4 | 0x10000u};
-}
-
-// Absorb one little-endian 32-bit word into the raw register.
-template <int TM>
-__device__ __forceinline__ uint32_t absorb(uint32_t crc, uint32_t w, LaneConst L, const uint32_t* tab) {
-    uint32_t x = crc ^ w;
-    if constexpr (TM == TM_S4R) {
-        uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
-        uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
-        uint32_t a2 = __builtin_amdgcn_perm(x, L.lc1, Sel<2>::v);
-        uint32_t a3 = __builtin_amdgcn_perm(x, L.lc1, Sel<3>::v);
-        return (ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1)) ^ (ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3));
-    } else if constexpr (TM == TM_S2R) {
-        uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
-        uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
-        uint32_t c = ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1) ^ (x >> 16);
-        uint32_t a2 = __builtin_amdgcn_perm(c, L.lc0, Sel<0>::v);
-        uint32_t a3 = __builtin_amdgcn_perm(c, L.lc0, Sel<1>::v);
-        return ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3) ^ (c >> 16);
-    } else {
-        return (tab[x & 0xffu] ^ tab[256 + ((x >> 8) & 0xffu)]) ^
-               (tab[512 + ((x >> 16) & 0xffu)] ^ tab[768 + (x >> 24)]);
-    }
-}
-
-template <int TM>
-__device__ __forceinline__ uint32_t absorb4(uint32_t crc, uint4 v, LaneConst L, const uint32_t* tab) {
-    crc = absorb<TM>(crc, v.x, L, tab);
-    crc = absorb<TM>(crc, v.y, L, tab);
-    crc = absorb<TM>(crc, v.z, L, tab);
-    crc = absorb<TM>(crc, v.w, L, tab);
-    return crc;
-}
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ldg4(const uint4* p) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint4 ldg4_plain(const uint4* p) { return *p; }
-
-// How a lane's 512-byte chunk reaches registers.
-enum LoadMode : int {
-    LM_DIRECT_NT = 0,     // lane loads its own chunk, nontemporal (64 lines per instruction)
-    LM_DIRECT = 1,        // same, default cache policy
-    LM_STAGED = 2,        // line-coalesced loads (8 whole lines per instruction) + LDS transpose
-};
-
-// Staging layout (one 8 KiB buffer per wave per round): piece t (16 B) of
-// owner lane i sits in slot t*64 + (i ^ t).  ds_write_b128 by the loading
-// lanes and ds_read_b128 by the owners are both bank-conflict-free.
-__device__ __forceinline__ uint32_t stage_slot(uint32_t owner, uint32_t t) { return t * 64u + (owner ^ t); }
-
-// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
-// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
-// Returns lane 0's first 16 bytes through *hdr.
-__device__ __forceinline__ void zero_header_bytes(uint4& v, bool l0, bool force_type, uint4* hdr) {
-    *hdr = v;
-    v.x = l0 ? 0u : v.x;
-    const uint32_t y = force_type ? ((v.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16)) : v.y;
-    v.y = l0 ? (y & 0xFFFF0000u) : v.y;
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
-// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
-// Returns lane 0's first 16 bytes through *hdr.
-template <int TM, int LM>
-__device__ __forceinline__ uint32_t full_block_lane_crc(const uint8_t* blk, LaneConst L, const uint32_t* tab,
-                                                        uint4* stage, uint4* hdr, bool force_type) {
-    const uint32_t lane = lane_id();
-    const bool l0 = lane == 0;
-    uint32_t crc = 0;
-    uint4 cur[8], nxt[8];
-    // Round r covers bytes [512 i + 128 r, +128) of every lane i.
-    auto load_round = [&](uint4* v, int r) {
-        if constexpr (LM == LM_STAGED) {
-            // instruction k: lanes 8m..8m+7 read the whole 128-B line of owner 8k+m
-            const uint8_t* base = blk + (lane >> 3) * 512u + r * 128 + (lane & 7u) * 16u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = ldg4(reinterpret_cast<const uint4*>(base + k * 8 * 512));
-        } else {
-            const uint4* p = reinterpret_cast<const uint4*>(blk + lane * 512u + r * 128);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = LM == LM_DIRECT_NT ? ldg4(p + j) : ldg4_plain(p + j);
-        }
-    };
-    load_round(cur, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        if (r < 3) load_round(nxt, r + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (LM == LM_STAGED) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) stage[stage_slot(8u * k + (lane >> 3), lane & 7u)] = cur[k];
-            wave_lds_sync();
-#pragma unroll
-            for (int t = 0; t < 8; ++t) cur[t] = stage[stage_slot(lane, t)];
-            wave_lds_sync();
-        }
-        if (r == 0) zero_header_bytes(cur[0], l0, force_type, hdr);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) crc = absorb4<TM>(crc, cur[j], L, tab);
-        __builtin_amdgcn_sched_barrier(0);
-        if (r < 3) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
-        }
-    }
-    return crc;
-}
-
-// ---------------------------------------------------------------------------
-// Config C2: one FULL record per block.
-// ---------------------------------------------------------------------------
-template <int TM, int THREADS, int LM, bool FRAME>
-__global__ __launch_bounds__(THREADS) void k_full_blocks(const uint8_t* __restrict__ blocks, uint64_t nblocks,
-                                                         uint32_t* __restrict__ masked_out,
-                                                         uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
-    __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
-    constexpr int kStageWaves = LM == LM_STAGED ? THREADS / 64 : 1;
-    __shared__ uint4 stage_all[kStageWaves][LM == LM_STAGED ? 512 : 1];
-    uint4* stage = stage_all[LM == LM_STAGED ? (threadIdx.x >> 6) : 0];
-    fill_tables<TM>(tab);
-    __syncthreads();
-    const LaneConst L = make_lane_const();
-    const uint32_t my_shift = c_lane_shift.c[lane_id()];
-    const uint64_t waves_per_wg = THREADS / 64;
-    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
-        const uint8_t* blk = blocks + b * kBlockSize;
-        uint4 hdr;
-        uint32_t r = full_block_lane_crc<TM, LM>(blk, L, tab, stage, &hdr, FRAME);
-        r = xor_reduce_wave(gf_mul(my_shift, r));
-        const uint32_t masked = mask(r ^ kFullInitXor);
-        if (lane_id() == 0) {
-            if constexpr (FRAME) {
-                // header [mask(crc) LE][len LE16][type]; byte 7 is payload.
-                uint2 h;
-                h.x = masked;
-                h.y = (hdr.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16) | kFullPayload;
-                *reinterpret_cast<uint2*>(frame_dst + b * kBlockSize) = h;
-            } else {
-                masked_out[b] = masked;
-                if (ok_out) {
-                    const bool ok = (hdr.x == masked) && ((hdr.y & 0xFFFFu) == kFullPayload) &&
-                                    (((hdr.y >> 16) & 0xFFu) == kFullTypeByte);
-                    ok_out[b] = ok ? 1 : 0;
-                }
-            }
-        }
-    }
-}
-
-// Read-only streaming ceiling with the same grid and block assignment:
-// coalesced 16 B/lane loads of the whole block, xor-folded, 4 B written.
-template <int THREADS>
-__global__ __launch_bounds__(THREADS) void k_stream_ceiling(const uint8_t* __restrict__ blocks, uint64_t nblocks,
-                                                            uint32_t* __restrict__ out) {
-    const uint64_t waves_per_wg = THREADS / 64;
-    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
-        const uint4* p = reinterpret_cast<const uint4*>(blocks + b * kBlockSize) + lane_id();
-        uint4 acc = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            uint4 v = ldg4(p + k * 64);
-            acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
-        }
-        uint32_t r = xor_reduce_wave(acc.x ^ acc.y ^ acc.z ^ acc.w);
-        if (lane_id() == 0) out[b] = r;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Synthetic C2 payloads: block b = splitmix64(seed ^ (first + b)) words.
-// ---------------------------------------------------------------------------
-__global__ void k_synth(uint64_t* __restrict__ dst, uint64_t nblocks, uint64_t seed, uint64_t first) {
-    const uint64_t words_per_block = kBlockSize / 8;
-    const uint64_t total = nblocks * words_per_block;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t b = i / words_per_block, w = i % words_per_block;
-        uint64_t z = (seed ^ (first + b)) + (w + 1) * 0x9E3779B97F4A7C15ull;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        dst[i] = z ^ (z >> 31);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Config C3: variable records (FULL/FIRST/MIDDLE/LAST mixes, padding, zeros).
-// ---------------------------------------------------------------------------
-struct Hdr {
-    uint32_t stored, len, type;
-};
-
-// Bytes [off, off+7) of a block of length bl, never reading at or past bl
-// (the image end need not be 4-byte aligned or padded).
-__device__ __forceinline__ Hdr read_header(const uint8_t* base, uint32_t off, uint32_t bl) {
-    const uint32_t a0 = off & ~3u;
-    uint32_t w0, w1, w2 = 0;
-    if (a0 + 12u <= bl) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(base + a0);
-        w0 = w[0]; w1 = w[1]; w2 = w[2];
-    } else {
-        uint8_t t[12];
-        for (uint32_t k = 0; k < 12; ++k) t[k] = a0 + k < bl ? base[a0 + k] : 0;
-        memcpy(&w0, t, 4); memcpy(&w1, t + 4, 4); memcpy(&w2, t + 8, 4);
-    }
-    const uint32_t sh = (off & 3u) * 8u;
-    const uint64_t lo = (uint64_t(w1) << 32) | w0;
-    const uint64_t hi = (uint64_t(w2) << 32) | w1;
-    const uint32_t a = uint32_t(lo >> sh);  // bytes off..off+3
-    const uint32_t b = uint32_t(hi >> sh);  // bytes off+4..off+7
-    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
-}
-
-// 16 bytes at block offset pos, zero outside [lo, bl) (lo > 0 only for the
-// first block of an image that starts mid-block).
-__device__ __forceinline__ uint4 load16_range(const uint8_t* blk, uint32_t pos, uint32_t lo, uint32_t bl) {
-    if (pos >= lo && pos + 16u <= bl) return ldg4_plain(reinterpret_cast<const uint4*>(blk + pos));
-    uint8_t t[16];
-    for (uint32_t k = 0; k < 16; ++k) t[k] = (pos + k >= lo && pos + k < bl) ? blk[pos + k] : 0;
-    uint4 v;
-    memcpy(&v, t, 16);
-    return v;
-}
-
-__device__ __forceinline__ Hdr read_header_range(const uint8_t* base, uint32_t off, uint32_t lo, uint32_t bl) {
-    if ((off & ~3u) >= lo) return read_header(base, off, bl);
-    uint8_t t[8];
-    for (uint32_t k = 0; k < 7; ++k) t[k] = base[off + k];  // off >= lo, off + 7 <= bl
-    t[7] = 0;
-    uint32_t a, b;
-    memcpy(&a, t, 4);
-    memcpy(&b, t + 4, 4);
-    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
-}
-
-// 16 bytes at block offset pos, zero past bl.
-__device__ __forceinline__ uint4 load16_guarded(const uint8_t* blk, uint32_t pos, uint32_t bl) {
-    if (pos + 16u <= bl) return ldg4(reinterpret_cast<const uint4*>(blk + pos));
-    uint8_t t[16];
-    for (uint32_t k = 0; k < 16; ++k) t[k] = pos + k < bl ? blk[pos + k] : 0;
-    uint4 v;
-    memcpy(&v, t, 16);
-    return v;
-}
-
-// One step of the physical-record walk (oracle walk_block rules).
-__device__ __forceinline__ uint32_t classify(const Hdr& h, uint32_t off, uint32_t bl) {
-    if (kHeaderSize + h.len > bl - off) return REVEL_REC_BAD_LENGTH;
-    if (h.type == 0 && h.len == 0) return REVEL_REC_ZERO;
-    return REVEL_REC_OK;
-}
-
-// Header-list entry: the 7 header bytes as read (stored CRC | len << 32 |
-// type << 48).  Offsets are not stored: entry k sits at the sum of 7 + len of
-// the entries before it (a wave prefix sum in the consumer).
-__device__ __forceinline__ uint64_t list_entry(const Hdr& h) {
-    return uint64_t(h.stored) | (uint64_t(h.len | (h.type << 16)) << 32);
-}
-__device__ __forceinline__ Hdr list_header(uint64_t e) {
-    const uint32_t hi = uint32_t(e >> 32);
-    return {uint32_t(e), hi & 0xFFFFu, (hi >> 16) & 0xFFu};
-}
-// Wave-wide exclusive prefix sum (lanes >= n contribute 0).
-__device__ __forceinline__ uint32_t wave_exclusive_sum(uint32_t v) {
-    uint32_t incl = v;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(incl, d, 64);
-        incl += lane_id() >= d ? t : 0u;
-    }
-    return incl - v;
-}
-
 // Per block (one lane each): number of physical records and, when list is
 // non-null, the first kListPerBlock headers (list_entry; the walk stops at the
 // first bad header, so only the last entry can be bad).
@@ -1270,136 +823,6 @@ __global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const 
 }
 
 // ---------------------------------------------------------------------------
-// Device replay reassembly (log_reader.rs:76-153, LevelDB-correct; the rules
-// of oracle LogReader / replay_events): physical records -> events in file
-// order: RECORD (FULL, or FIRST MIDDLE* LAST all valid) or ERROR (zero record,
-// length past the block that is not the torn tail of the image, checksum
-// mismatch when checking, unknown type).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool reasm_is_error(const revel_record_result& r, bool checksum, bool tail) {
-    if (r.status == REVEL_REC_ZERO) return true;
-    if (r.status == REVEL_REC_BAD_LENGTH) return !tail;
-    if (checksum && r.status == REVEL_REC_BAD_CHECKSUM) return true;
-    return r.type < REVEL_FULL_TYPE || r.type > REVEL_LAST_TYPE;
-}
-
-__global__ void k_reasm_classify(const revel_record_result* __restrict__ phys, uint64_t n, uint64_t image_end,
-                                 int checksum, uint32_t* __restrict__ ev_flag, uint64_t* __restrict__ ev_len,
-                                 uint32_t* __restrict__ ev_end) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const revel_record_result r = phys[i];
-        auto tail_of = [&](uint64_t k, const revel_record_result& q) {
-            return k == n - 1 && q.status == REVEL_REC_BAD_LENGTH && q.file_offset + kHeaderSize + q.length > image_end;
-        };
-        uint32_t flag = 0, end = (uint32_t)i;
-        uint64_t len = 0;
-        const bool tail = tail_of(i, r);
-        if (reasm_is_error(r, checksum, tail)) {
-            flag = 1;  // ERROR event
-        } else if (!tail) {
-            if (r.type == REVEL_FULL_TYPE) {
-                flag = 1;
-                len = r.length;
-            } else if (r.type == REVEL_FIRST_TYPE) {
-                uint64_t acc = r.length;
-                for (uint64_t j = i + 1; j < n; ++j) {
-                    const revel_record_result q = phys[j];
-                    if (reasm_is_error(q, checksum, tail_of(j, q)) || tail_of(j, q)) break;
-                    if (q.type == REVEL_MIDDLE_TYPE) {
-                        acc += q.length;
-                        continue;
-                    }
-                    if (q.type == REVEL_LAST_TYPE) {
-                        flag = 1;
-                        len = acc + q.length;
-                        end = (uint32_t)j;
-                    }
-                    break;  // FULL / FIRST: this fragment is dropped
-                }
-            }
-        }
-        ev_flag[i] = flag;
-        ev_len[i] = len;
-        ev_end[i] = end;
-    }
-}
-
-__global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint64_t n, uint64_t image_end, int checksum,
-                             const uint32_t* __restrict__ ev_flag, const uint32_t* __restrict__ ev_idx,
-                             const uint64_t* __restrict__ pay_off, const uint32_t* __restrict__ ev_end,
-                             revel_logical_record* __restrict__ out, uint64_t* __restrict__ frag_dst) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        if (!ev_flag[i]) continue;
-        const revel_record_result r = phys[i];
-        const bool tail = i == n - 1 && r.status == REVEL_REC_BAD_LENGTH &&
-                          r.file_offset + kHeaderSize + r.length > image_end;
-        revel_logical_record o;
-        o.file_offset = r.file_offset;
-        o.payload_offset = pay_off[i];
-        o.first_phys = (uint32_t)i;
-        o.last_phys = ev_end[i];
-        o.reserved[0] = o.reserved[1] = o.reserved[2] = 0;
-        if (reasm_is_error(r, checksum, tail)) {
-            o.length = 0;
-            o.status = r.status == REVEL_REC_OK || (!checksum && r.status == REVEL_REC_BAD_CHECKSUM)
-                           ? REVEL_LOGICAL_BAD_TYPE
-                           : r.status;
-        } else {
-            uint64_t acc = 0;
-            for (uint64_t k = i; k <= ev_end[i]; ++k) {
-                frag_dst[k] = pay_off[i] + acc;
-                acc += phys[k].length;
-            }
-            o.length = (uint32_t)acc;
-            o.status = REVEL_LOGICAL_OK;
-        }
-        out[ev_idx[i]] = o;
-    }
-}
-
-// One wave copies len bytes src -> dst, any byte alignment of either: a byte
-// head up to dst's next 16-B boundary, then aligned 16-B stores whose source
-// bytes are funnel-shifted (v_alignbyte) out of 4-B-aligned dword loads (never
-// reading past the source range), then a byte tail.  Coalesced both ways.
-__device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
-    const uint32_t lane = lane_id();
-    const uint32_t head = min(len, (16u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
-    if (lane < head) dst[lane] = src[lane];
-    const uint8_t* s = src + head;
-    uint8_t* d = dst + head;
-    const uint32_t n = len - head;
-    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
-    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s - sh);
-    // vector v reads s4[4v .. 4v+3] (+ s4[4v+4] when sh != 0): stay inside [s, s+n)
-    const uint32_t nvec = sh == 0 ? n / 16u : (n + sh >= 20u ? (n + sh - 20u) / 16u + 1u : 0u);
-    for (uint32_t v = lane; v < nvec; v += 64) {
-        const uint32_t* q = s4 + 4u * v;
-        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = sh ? q[4] : 0u;
-        uint4 o;
-        o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
-        o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
-        *reinterpret_cast<uint4*>(d + 16u * v) = o;
-    }
-    for (uint32_t i = nvec * 16u + lane; i < n; i += 64) d[i] = s[i];
-}
-
-// One wave per physical record that belongs to an emitted logical record.
-__global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image_base,
-                               const revel_record_result* __restrict__ phys, uint64_t n,
-                               const uint64_t* __restrict__ frag_dst, uint8_t* __restrict__ payload) {
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-    const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint64_t k = w0; k < n; k += waves) {
-        const uint64_t dst = frag_dst[k];
-        if (dst == ~0ull) continue;
-        const revel_record_result r = phys[k];
-        wave_copy(image + (r.file_offset - image_base) + kHeaderSize, payload + dst, r.length);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Per-window verdict summaries for the end-to-end replay: units, bad units and
 // the smallest bad file offset (summary[0..2]; reset by the host to 0,0,~0).
 // ---------------------------------------------------------------------------
@@ -1437,405 +860,9 @@ __global__ void k_summary_blocks(const uint8_t* __restrict__ ok, uint64_t nblock
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&summary[0], (unsigned long long)nblocks);
 }
 
-// ---------------------------------------------------------------------------
-// Launch helpers
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// Config C2, v2: software-pipelined across blocks, CHAINS independent CRC
-// chains per lane (lane i's 512-byte chunk split into CHAINS contiguous
-// sub-chunks that advance in lockstep), and the GF(2) combine done either by
-// a per-lane multiply (EPI_GFMUL) or by a table-driven shift tree (EPI_TREE).
-// ---------------------------------------------------------------------------
-enum Epilogue : int { EPI_GFMUL = 0, EPI_TREE = 1 };
-
-// x^(8 * 256 * 2^L) mod P, L = 0..6: the shift applied at tree level L.
-struct TreeShiftConsts {
-    uint32_t c[7];
-};
-constexpr TreeShiftConsts make_tree_shift() {
-    TreeShiftConsts t{};
-    for (int L = 0; L < 7; ++L) t.c[L] = x8n(256ull << L);
-    return t;
-}
-__constant__ TreeShiftConsts c_tree_shift = make_tree_shift();
-constexpr uint32_t kShift256 = x8n(256);
-
-// shift tables: level L, byte k, entry e at shtab[L*1024 + k*256 + e] =
-// (e << 8k) * x^(8 * 256 * 2^L) mod P.
-__device__ void fill_shift_tables(uint32_t* shtab, int levels) {
-    for (uint32_t d = threadIdx.x; d < uint32_t(levels) * 1024u; d += blockDim.x) {
-        const uint32_t L = d >> 10, k = (d >> 8) & 3u, e = d & 255u;
-        shtab[d] = gf_mul(c_tree_shift.c[L], e << (8u * k));
-    }
-}
-
-template <int L>
-__device__ __forceinline__ uint32_t tree_shift(const uint32_t* shtab, uint32_t v) {
-    const uint32_t* t = shtab + L * 1024;
-    return (t[v & 0xffu] ^ t[256 + ((v >> 8) & 0xffu)]) ^ (t[512 + ((v >> 16) & 0xffu)] ^ t[768 + (v >> 24)]);
-}
-
-template <int TM, int THREADS, int CHAINS, int EPI, bool FRAME>
-__global__ __launch_bounds__(THREADS) void k_full_blocks2(const uint8_t* __restrict__ blocks, uint64_t nblocks,
-                                                          uint32_t* __restrict__ masked_out,
-                                                          uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
-    static_assert(CHAINS == 1 || CHAINS == 2, "chains");
-    constexpr int kLevels = EPI == EPI_TREE ? 7 : 0;
-    constexpr int kL0 = 1;  // lane-tree level lv uses table lv + 1 (shift 512 * 2^lv)
-    __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
-    __shared__ uint32_t shtab[kLevels ? kLevels * 1024 : 1];
-    fill_tables<TM>(tab);
-    if constexpr (kLevels > 0) fill_shift_tables(shtab, kLevels);
-    __syncthreads();
-    const LaneConst L = make_lane_const();
-    const uint32_t lane = lane_id();
-    const bool l0 = lane == 0;
-    const uint32_t my_shift = c_lane_shift.c[lane];
-    const uint64_t waves_per_wg = THREADS / 64;
-    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-
-    // round r of block b: CHAINS=1 -> bytes [512i + 128r, +128);
-    // CHAINS=2 -> chain A [512i + 64r, +64) in v[0..3], chain B [512i + 256 + 64r, +64) in v[4..7]
-    auto load_round = [&](uint4* v, uint64_t b, int r) {
-        const uint8_t* base = blocks + b * kBlockSize + lane * 512u;
-        if constexpr (CHAINS == 1) {
-            const uint4* p = reinterpret_cast<const uint4*>(base + r * 128);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(p + j);
-        } else {
-            const uint4* pa = reinterpret_cast<const uint4*>(base + r * 64);
-            const uint4* pb = reinterpret_cast<const uint4*>(base + 256 + r * 64);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = ldg4_plain(pa + j);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[4 + j] = ldg4_plain(pb + j);
-        }
-    };
-
-    uint4 cur[8], nxt[8];
-    uint64_t b = gwave;
-    if (b < nblocks) load_round(cur, b, 0);
-    for (; b < nblocks; b += nwaves) {
-        uint32_t ca = 0, cb = 0;
-        uint4 hdr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (r < 3) {
-                load_round(nxt, b, r + 1);
-            } else if (b + nwaves < nblocks) {
-                load_round(nxt, b + nwaves, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (r == 0) zero_header_bytes(cur[0], l0, FRAME, &hdr);
-            if constexpr (CHAINS == 1) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ca = absorb4<TM>(ca, cur[j], L, tab);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    ca = absorb4<TM>(ca, cur[j], L, tab);
-                    cb = absorb4<TM>(cb, cur[4 + j], L, tab);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
-        }
-        // ---- combine: R(block) = XOR_i R_i * x^(8*512*(63-i)) ----
-        uint32_t raw;
-        if constexpr (EPI == EPI_GFMUL) {
-            uint32_t v = CHAINS == 2 ? (gf_mul(kShift256, ca) ^ cb) : ca;
-            raw = xor_reduce_wave(gf_mul(my_shift, v));
-        } else {
-            uint32_t v = ca;
-            if constexpr (CHAINS == 2) v = tree_shift<0>(shtab, ca) ^ cb;
-#pragma unroll
-            for (int lv = 0; lv < 6; ++lv) {
-                uint32_t sft;
-                switch (lv) {  // table level = lane-tree level + kL0
-                    case 0: sft = tree_shift<kL0 + 0>(shtab, v); break;
-                    case 1: sft = tree_shift<kL0 + 1>(shtab, v); break;
-                    case 2: sft = tree_shift<kL0 + 2>(shtab, v); break;
-                    case 3: sft = tree_shift<kL0 + 3>(shtab, v); break;
-                    case 4: sft = tree_shift<kL0 + 4>(shtab, v); break;
-                    default: sft = tree_shift<kL0 + 5>(shtab, v); break;
-                }
-                const uint32_t up = __shfl_up(sft, 1u << lv, 64);
-                const uint32_t m = (2u << lv) - 1u;
-                v = ((lane & m) == m) ? (v ^ up) : v;
-            }
-            raw = __builtin_amdgcn_readlane(v, 63);
-        }
-        const uint32_t masked = mask(raw ^ kFullInitXor);
-        if (l0) {
-            if constexpr (FRAME) {
-                uint2 h;
-                h.x = masked;
-                h.y = (hdr.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16) | kFullPayload;
-                *reinterpret_cast<uint2*>(frame_dst + b * kBlockSize) = h;
-            } else {
-                masked_out[b] = masked;
-                if (ok_out) {
-                    const bool ok = (hdr.x == masked) && ((hdr.y & 0xFFFFu) == kFullPayload) &&
-                                    (((hdr.y >> 16) & 0xFFu) == kFullTypeByte);
-                    ok_out[b] = ok ? 1 : 0;
-                }
-            }
-        }
-    }
-}
-
-template <int TM, int THREADS, int CHAINS, int EPI, bool FRAME>
-hipError_t launch_full2(const DeviceInfo& di, const uint8_t* blocks, uint64_t n, uint32_t* masked, uint8_t* ok,
-                        uint8_t* frame_dst, hipStream_t st) {
-    auto kern = k_full_blocks2<TM, THREADS, CHAINS, EPI, FRAME>;
-    const uint64_t wg_needed = (n + THREADS / 64 - 1) / (THREADS / 64);
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, wg_needed));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked, ok, frame_dst);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Config C2, v3: interleaved word streams with the gap folded into the tables.
-//
-// Stream s (s = 0..255) is the 32-bit words at byte offsets 4s + 1024k,
-// k = 0..31; lane i owns streams 4i..4i+3, i.e. one 16-byte load per lane
-// per 1 KiB: exactly the coalescing of a plain streaming read (1 KiB per
-// wave instruction).  Consecutive words of a stream are 1024 bytes apart, so
-// with tables T''m = x^(8*1020) * Tm the chain
-//     U <- T''3[x0] ^ T''2[x1] ^ T''1[x2] ^ T''0[x3],   x = U ^ w
-// absorbs a word AND the 1020 bytes of other streams' data that follow it in
-// one step (shifting is linear, so it distributes over the table xor).  The
-// four streams of a lane are four independent chains (ILP 4).  After its 32nd
-// word, stream s stands at byte 32768 + 4s; the block register is
-//     R = XOR_s  U_s * x^(-32 s)  mod P
-// (x is invertible mod P since P(0) = 1), evaluated by an 8-level tree of
-// inverse-shift tables: 2 levels inside the lane, 6 across lanes.
-// ---------------------------------------------------------------------------
-struct GapTables {
-    uint32_t t[4][256];  // t[m][e] = x^(8*1020) * T_m[e]
-};
-constexpr GapTables make_gap_tables() {
-    GapTables g{};
-    const SliceTables st = make_slice_tables();
-    const uint32_t c = x8n(1020);
-    for (int m = 0; m < 4; ++m)
-        for (int e = 0; e < 256; ++e) g.t[m][e] = multmodp(c, st.t[m][e]);
-    return g;
-}
-__constant__ GapTables c_gap = make_gap_tables();
-
-constexpr uint32_t pow_modp(uint32_t a, uint64_t n) {
-    uint32_t r = 0x80000000u;
-    while (n) {
-        if (n & 1u) r = multmodp(r, a);
-        a = multmodp(a, a);
-        n >>= 1;
-    }
-    return r;
-}
-constexpr uint32_t kXInv = 0x05EC76F1u;  // x^-1 mod P, reflected
-static_assert(multmodp(kXInv, 0x40000000u) == 0x80000000u, "x * x^-1 == 1");
-// x^(-8 * 4 * 2^L): tree level L combines streams 2^L apart (4 * 2^L bytes)
-struct InvTreeConsts {
-    uint32_t c[8];
-};
-constexpr InvTreeConsts make_inv_tree() {
-    InvTreeConsts t{};
-    for (int L = 0; L < 8; ++L) t.c[L] = pow_modp(kXInv, 8ull * 4ull * (1ull << L));
-    return t;
-}
-__constant__ InvTreeConsts c_inv_tree = make_inv_tree();
-static_assert(multmodp(make_inv_tree().c[0], x8n(4)) == 0x80000000u, "inverse shift");
-
-__device__ void fill_gap_tables(uint32_t* tab) {
-    // S4R layout; byte0 -> T''3 (r0 h0), byte1 -> T''2 (r0 h1), byte2 -> T''1 (r1 h0), byte3 -> T''0 (r1 h1)
-    for (uint32_t d = threadIdx.x; d < 32768u; d += blockDim.x) {
-        const uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
-        tab[d] = c_gap.t[3 - (r * 2 + h)][e];
-    }
-}
-__device__ void fill_inv_tree_tables(uint32_t* shtab) {
-    for (uint32_t d = threadIdx.x; d < 8u * 1024u; d += blockDim.x) {
-        const uint32_t L = d >> 10, k = (d >> 8) & 3u, e = d & 255u;
-        shtab[d] = gf_mul(c_inv_tree.c[L], e << (8u * k));
-    }
-}
-
-template <bool NT>
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-    return NT ? ldg4(reinterpret_cast<const uint4*>(p)) : ldg4_plain(reinterpret_cast<const uint4*>(p));
-}
-
-template <int THREADS, bool NT, bool FRAME>
-__global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restrict__ blocks, uint64_t nblocks,
-                                                          uint32_t* __restrict__ masked_out,
-                                                          uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
-    __shared__ uint32_t tab[32768];      // 128 KiB: T'' replicated 32x
-    __shared__ uint32_t shtab[8 * 1024];  // 32 KiB: inverse-shift tree tables
-    fill_gap_tables(tab);
-    fill_inv_tree_tables(shtab);
-    __syncthreads();
-    const LaneConst L = make_lane_const();
-    const uint32_t lane = lane_id();
-    const bool l0 = lane == 0;
-    const uint64_t waves_per_wg = THREADS / 64;
-    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-
-    // round r (0..3) of block b: words of the 8 KiB [8192 r, +8192); lane i
-    // loads 16 B at 1024 k + 16 i, k = 0..7
-    auto load_round = [&](uint4* v, uint64_t b, int r) {
-        const uint8_t* base = blocks + b * kBlockSize + r * 8192 + lane * 16u;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = ld16<NT>(base + k * 1024);
-    };
-
-    uint4 cur[8], nxt[8];
-    uint64_t b = gwave;
-    if (b < nblocks) load_round(cur, b, 0);
-    for (; b < nblocks; b += nwaves) {
-        uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-        uint4 hdr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (r < 3) {
-                load_round(nxt, b, r + 1);
-            } else if (b + nwaves < nblocks) {
-                load_round(nxt, b + nwaves, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (r == 0) zero_header_bytes(cur[0], l0, FRAME, &hdr);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                u0 = absorb<TM_S4R>(u0, cur[k].x, L, tab);
-                u1 = absorb<TM_S4R>(u1, cur[k].y, L, tab);
-                u2 = absorb<TM_S4R>(u2, cur[k].z, L, tab);
-                u3 = absorb<TM_S4R>(u3, cur[k].w, L, tab);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
-        }
-        // ---- tree combine: R = XOR_s U_s x^(-32 s) ----
-        uint32_t v0 = u0 ^ tree_shift<0>(shtab, u1);
-        uint32_t v1 = u2 ^ tree_shift<0>(shtab, u3);
-        uint32_t v = v0 ^ tree_shift<1>(shtab, v1);
-#pragma unroll
-        for (int lv = 0; lv < 6; ++lv) {
-            uint32_t t;
-            switch (lv) {
-                case 0: t = tree_shift<2>(shtab, v); break;
-                case 1: t = tree_shift<3>(shtab, v); break;
-                case 2: t = tree_shift<4>(shtab, v); break;
-                case 3: t = tree_shift<5>(shtab, v); break;
-                case 4: t = tree_shift<6>(shtab, v); break;
-                default: t = tree_shift<7>(shtab, v); break;
-            }
-            const uint32_t dn = __shfl_down(t, 1u << lv, 64);
-            const uint32_t m = (2u << lv) - 1u;
-            v = ((lane & m) == 0u) ? (v ^ dn) : v;
-        }
-        const uint32_t raw = __builtin_amdgcn_readfirstlane(v);
-        const uint32_t masked = mask(raw ^ kFullInitXor);
-        if (l0) {
-            if constexpr (FRAME) {
-                uint2 h;
-                h.x = masked;
-                h.y = (hdr.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16) | kFullPayload;
-                *reinterpret_cast<uint2*>(frame_dst + b * kBlockSize) = h;
-            } else {
-                masked_out[b] = masked;
-                if (ok_out) {
-                    const bool ok = (hdr.x == masked) && ((hdr.y & 0xFFFFu) == kFullPayload) &&
-                                    (((hdr.y >> 16) & 0xFFu) == kFullTypeByte);
-                    ok_out[b] = ok ? 1 : 0;
-                }
-            }
-        }
-    }
-}
-
-template <int THREADS, bool NT, bool FRAME>
-hipError_t launch_full3(const DeviceInfo& di, const uint8_t* blocks, uint64_t n, uint32_t* masked, uint8_t* ok,
-                        uint8_t* frame_dst, hipStream_t st) {
-    auto kern = k_full_blocks3<THREADS, NT, FRAME>;
-    const uint64_t wg_needed = (n + THREADS / 64 - 1) / (THREADS / 64);
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, wg_needed));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked, ok, frame_dst);
-    return hipGetLastError();
-}
-
-template <int TM, int THREADS, int LM, bool FRAME>
-hipError_t launch_full(const DeviceInfo& di, int wg_per_cu, const uint8_t* blocks, uint64_t n, uint32_t* masked,
-                       uint8_t* ok, uint8_t* frame_dst, hipStream_t st) {
-    auto kern = k_full_blocks<TM, THREADS, LM, FRAME>;
-    const uint64_t waves_needed = n;
-    uint64_t grid = (uint64_t)di.num_cu * wg_per_cu;
-    const uint64_t wg_needed = (waves_needed + THREADS / 64 - 1) / (THREADS / 64);
-    grid = std::max<uint64_t>(1, std::min(grid, wg_needed));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked, ok, frame_dst);
-    return hipGetLastError();
-}
-
 }  // namespace
 
-// ===========================================================================
-// Internal entry points (declared in gpu_internal.h)
-// ===========================================================================
 namespace revel {
-
-// Variant table used by the public entry point and by tools/variants.py.
-hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void* d_blocks, uint64_t n,
-                                   uint32_t* d_masked, uint8_t* d_ok, hipStream_t st) {
-    const uint8_t* b = static_cast<const uint8_t*>(d_blocks);
-    switch (variant) {
-        // production: v3 interleaved word streams (gap-folded tables), nt loads
-        case 0: return launch_full3<1024, true, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 9: return launch_full<TM_S4R, 1024, LM_DIRECT, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
-        case 8: return launch_full<TM_S2R, 768, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
-        // v2 (pipelined across blocks): chains x epilogue
-        case 10: return launch_full2<TM_S4R, 1024, 1, EPI_GFMUL, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 11: return launch_full2<TM_S4R, 1024, 2, EPI_GFMUL, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 12: return launch_full2<TM_S4R, 1024, 1, EPI_TREE, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 13: return launch_full2<TM_S4R, 1024, 2, EPI_TREE, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 14: return launch_full2<TM_S2R, 1024, 2, EPI_TREE, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        // v3: interleaved word streams, gap folded into the tables
-        case 20: return launch_full3<1024, true, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 21: return launch_full3<1024, false, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        case 1: return launch_full<TM_S2R, 512, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
-        case 2: return launch_full<TM_S4R, 256, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
-        case 3: return launch_full<TM_S4, 1024, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
-        case 4: return launch_full<TM_S2R, 512, LM_DIRECT, false>(di, 2, b, n, d_masked, d_ok, nullptr, st);
-        case 5: return launch_full<TM_S4R, 1024, LM_DIRECT, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
-        case 6: return launch_full<TM_S4, 512, LM_DIRECT, false>(di, 4, b, n, d_masked, d_ok, nullptr, st);
-        case 7: return launch_full<TM_S2R, 512, LM_DIRECT_NT, false>(di, 2, b, n, d_masked, d_ok, nullptr, st);
-        case 100: {
-            const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 3) / 4));
-            hipLaunchKernelGGL(k_stream_ceiling<256>, dim3((uint32_t)grid), dim3(256), 0, st, b, n, d_masked);
-            return hipGetLastError();
-        }
-        default: return hipErrorInvalidValue;
-    }
-}
-
-hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st) {
-    uint8_t* b = static_cast<uint8_t*>(d_blocks);
-    return launch_full3<1024, true, true>(di, b, n, nullptr, nullptr, b, st);
-}
-
-hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
-                             hipStream_t st) {
-    const uint64_t words = n * (kBlockSize / 8);
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 16, (words + 255) / 256));
-    hipLaunchKernelGGL(k_synth, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<uint64_t*>(d_blocks), n, seed,
-                       first);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return frame_full_blocks(di, d_blocks, n, st);
-}
-
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
@@ -1988,32 +1015,6 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const bool partial = lead != 0 || (image_len + lead) % kBlockSize != 0;
     return launch_verify3<true>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr,
                                 lead, nullptr, nullptr, st);
-}
-
-hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
-                          int checksum, uint32_t* d_flag, uint64_t* d_len, uint32_t* d_end, hipStream_t st) {
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));
-    hipLaunchKernelGGL(k_reasm_classify, dim3((uint32_t)grid), dim3(256), 0, st, d_phys, n, image_end, checksum, d_flag,
-                       d_len, d_end);
-    return hipGetLastError();
-}
-
-hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
-                      int checksum, const uint32_t* d_flag, const uint32_t* d_idx, const uint64_t* d_off,
-                      const uint32_t* d_end, revel_logical_record* d_out, uint64_t* d_frag_dst, hipStream_t st) {
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));
-    hipLaunchKernelGGL(k_reasm_emit, dim3((uint32_t)grid), dim3(256), 0, st, d_phys, n, image_end, checksum, d_flag,
-                       d_idx, d_off, d_end, d_out, d_frag_dst);
-    return hipGetLastError();
-}
-
-hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
-                        const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
-                        hipStream_t st) {
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 3) / 4));
-    hipLaunchKernelGGL(k_reasm_gather, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<const uint8_t*>(d_image),
-                       image_base, d_phys, n, d_frag_dst, static_cast<uint8_t*>(d_payload));
-    return hipGetLastError();
 }
 
 }  // namespace revel
