@@ -171,7 +171,7 @@ int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t 
         if (ctx->hlist) (void)hipFree(ctx->hlist);
         ctx->hlist = nullptr;
         ctx->hlist_cap_blocks = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->hlist), nblocks * revel::kListPerBlock * sizeof(uint64_t)),
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->hlist), nblocks * revel::kListStride * sizeof(uint64_t)),
                 "hipMalloc(header list)");
         ctx->hlist_cap_blocks = nblocks;
     }

@@ -15,7 +15,8 @@ using namespace revel;
 namespace {
 // Per block (one lane each): number of physical records and, when list is
 // non-null, the first kListPerBlock headers (list_entry; the walk stops at the
-// first bad header, so only the last entry can be bad).
+// first bad header, so only the last entry can be bad) followed by the in-block
+// offset of record kListPerBlock when the block has more records.
 __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts,
                                 uint64_t* __restrict__ hlist) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
@@ -28,12 +29,39 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
         while (bl - off >= kHeaderSize) {
             const Hdr h = read_header(blk, off, bl);
             const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-            if (hlist && n < kListPerBlock) hlist[b * kListPerBlock + n] = list_entry(h);
+            if (hlist && n < kListPerBlock) hlist[b * kListStride + n] = list_entry(h);
+            if (hlist && n == kListPerBlock) hlist[b * kListStride + kListPerBlock] = off;  // resume point
             ++n;
             if (!ok) break;
             off += kHeaderSize + h.len;
         }
         counts[b] = n;
+    }
+}
+
+// Header-list entries of records kListPerBlock.. of the blocks that have more
+// (small-record logs: a 131-B record gives ~250 per block), one lane per block,
+// resuming at the offset the count pass left.  Entry k of block b goes into the
+// first 8 bytes of its own 24-byte result slot out[first[b] + k]: the verify
+// pass that covers record k reads it before it writes the result there.
+__global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbytes, const uint32_t* __restrict__ counts,
+                                const uint32_t* __restrict__ first, const uint64_t* __restrict__ hlist,
+                                revel_record_result* __restrict__ out) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t n = counts[b];
+        if (n <= kListPerBlock) continue;
+        const uint64_t base = b * kBlockSize;
+        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
+        const uint8_t* blk = image + base;
+        uint32_t off = (uint32_t)hlist[b * kListStride + kListPerBlock];
+        uint64_t* slot = reinterpret_cast<uint64_t*>(out + first[b]);
+        for (uint32_t k = kListPerBlock; k < n; ++k) {
+            const Hdr h = read_header(blk, off, bl);
+            slot[k * (sizeof(revel_record_result) / 8)] = list_entry(h);
+            off += kHeaderSize + h.len;  // only the last record can be bad
+        }
     }
 }
 
@@ -407,7 +435,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
         const uint32_t nlist = (hlist && counts) ? counts[b] : kNone;
         for (;;) {
             if (walk_from == lo_b && nlist <= kListPerBlock) {
-                const Hdr h = list_header(lane < nlist ? hlist[b * kListPerBlock + lane] : 0ull);
+                const Hdr h = list_header(lane < nlist ? hlist[b * kListStride + lane] : 0ull);
                 const uint32_t off = lo_b + wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
                 if (lane < nlist) {
                     const bool bad = classify(h, off, bl) != REVEL_REC_OK;
@@ -613,18 +641,19 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     uint4 cur[8], nxt[8];
     uint32_t pf_count = kNone, pf_first = 0;
     uint64_t pf_hl = 0;
-    auto load_round = [&](const uint8_t* blk, uint4* v, int rr) {
+    auto load_round = [&](const uint8_t* blk, uint4* v, int rr, bool own, uint32_t cs_ref) {
+        const uint8_t* p = blk + (own ? cs : cs_ref) + rr * 128;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + rr * 128 + j * 16));
+        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 16));
     };
     // header list first: the list is needed before the data (loads return in order)
     auto prefetch = [&](uint64_t nb) {
         if (use_list) {
             pf_count = counts[nb];
-            pf_hl = hlist[nb * kListPerBlock + lane];
+            pf_hl = hlist[nb * kListStride + lane];
         }
         if constexpr (!FRAME) pf_first = first[nb];
-        load_round(image + nb * kBlockSize - lead, cur, 0);
+        load_round(image + nb * kBlockSize - lead, cur, 0, true, 0u);
     };
     prefetch(b);
     while (b < b_hi) {
@@ -632,18 +661,24 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
         const uint8_t* blk = image + base - lead;
         const uint64_t bn = b + nwaves;
         const uint32_t nlist = pf_count;
-        const uint64_t hl_e = pf_hl;
+        uint64_t ent = pf_hl;  // this lane's header-list entry of the current batch
+        const uint32_t first_b = __builtin_amdgcn_readfirstlane(pf_first);
         uint32_t out_base = pf_first;
-        uint32_t walk_from = 0;
+        uint32_t walk_from = 0;              // header walk (no list given)
+        uint32_t lpass = 0, lpass_off = 0;   // list passes: records [64 lpass, +64), first header offset
         bool have_round0 = true;
         for (;;) {
-            const bool from_list = walk_from == 0 && nlist <= kListPerBlock;
+            const bool from_list = use_list;
             if (from_list) {
-                // headers come from the count pass; offsets by prefix sum; the
-                // finalizer reads them back from LDS (no global header reads)
-                const Hdr h = list_header(hl_e);
-                const uint32_t off = wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
-                if (lane < nlist) {
+                // headers come from the count pass (the first kListPerBlock) or
+                // from k_list_overflow (the rest, in this block's result slots);
+                // offsets by prefix sum; the finalizer reads them back from LDS
+                const uint32_t k0 = lpass * kListPerBlock;
+                const uint32_t np = min(nlist - k0, kListPerBlock);
+                const Hdr h = list_header(ent);
+                const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
+                const uint32_t off = lpass_off + wave_exclusive_sum(sz);
+                if (lane < np) {
                     const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
                     wl.off[lane] = (uint16_t)off;
                     wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
@@ -653,10 +688,11 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                     wl.hlt[lane] = h.len | (h.type << 16);
                 }
                 if (lane == 0) {
-                    wl.s[nlist] = wl.em1[nlist] = kNoRange;
-                    wl.nrec = nlist;
-                    wl.more_off = kNone;
+                    wl.s[np] = wl.em1[np] = kNoRange;
+                    wl.nrec = np;
+                    wl.more_off = k0 + np < nlist ? 1u : kNone;
                 }
+                lpass_off = __builtin_amdgcn_readlane(off + sz, np - 1u);  // header offset of the next pass
             } else if (lane == 0) {
                 uint32_t off = walk_from, n = 0, cont = kNone;
                 while (kBlockSize - off >= kHeaderSize) {
@@ -692,11 +728,16 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             load_rec(r, s, e);
             const bool active = r < nrec && s < ce;
             uint32_t state = 0;
-            if (__any(active)) {
-                if (!have_round0) load_round(blk, cur, 0);
+            const uint64_t act_mask = __ballot(active);
+            if (act_mask) {
+                // lanes with no record of this batch in their chunk load an
+                // active lane's addresses instead (same lines, no traffic):
+                // a block listed in several batches is not re-read whole
+                const uint32_t cs_ref = (uint32_t)__builtin_ctzll(act_mask) * 512u;  // wave-uniform
+                if (!have_round0) load_round(blk, cur, 0, active, cs_ref);
 #pragma unroll 1
                 for (int rr = 0; rr < 4; ++rr) {
-                    if (rr < 3) load_round(blk, nxt, rr + 1);
+                    if (rr < 3) load_round(blk, nxt, rr + 1, active, cs_ref);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
@@ -786,7 +827,15 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             out_base += nrec;
             wave_lds_sync();
             if (cont == kNone) break;
-            walk_from = cont;
+            if (from_list) {
+                ++lpass;
+                if constexpr (!FRAME) {
+                    const uint32_t k0 = lpass * kListPerBlock;
+                    ent = k0 + lane < nlist ? *reinterpret_cast<const uint64_t*>(out + first_b + k0 + lane) : 0ull;
+                }
+            } else {
+                walk_from = cont;
+            }
         }
         b = bn;
     }
@@ -915,6 +964,15 @@ template <bool FRAME>
 static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                  uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
+    if (!FRAME && hl && d_counts) {
+        // list the headers of blocks with more than kListPerBlock records
+        const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
+        hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
+                           d_out);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL((k_verify_records3<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();

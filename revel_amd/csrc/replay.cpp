@@ -89,7 +89,7 @@ int ring_init(Ring& R, int nbuf) {
         if (R.mode == REVEL_REPLAY_RECORDS) {
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_counts), nblocks * 4), "hipMalloc(counts)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_first), nblocks * 4), "hipMalloc(first)");
-            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), nblocks * revel::kListPerBlock * 8), "hipMalloc(hlist)");
+            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), nblocks * revel::kListStride * 8), "hipMalloc(hlist)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_scan), revel::scan_scratch_words(nblocks) * 4), "hipMalloc(scan)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_res), nblocks * kMaxRecordsPerBlock * sizeof(revel_record_result)),
                 "hipMalloc(records)");

@@ -191,6 +191,38 @@ def test_verify_small_records_dense(gpu_ctx):
         compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), oc.walk(img))
 
 
+@pytest.mark.parametrize("rec_len", [24, 100, 124, 200])
+def test_verify_multi_batch_lists(gpu_ctx, rec_len):
+    """Blocks with 2..10 header-list batches of 64 records (the count pass
+    lists 64, k_list_overflow the rest): bit flips in every batch, a zero
+    record and a bad length deep in a block, all parity-checked."""
+    rng = np.random.default_rng(rec_len)
+    recs = [rng.integers(0, 256, rec_len + int(rng.integers(0, 8)), dtype=np.uint8).tobytes()
+            for _ in range(6 * BLOCK_SIZE // (rec_len + 7))]
+    img = bytearray(oc.write_image(recs))
+    ref = oc.walk(bytes(img))
+    # one flip per 37 records: every 64-record batch of every block gets some
+    for v in range(5, len(ref) - 1, 37):
+        off = int(ref["file_offset"][v]) + 7 + int(rng.integers(0, int(ref["length"][v])))
+        img[off] ^= 1 << int(rng.integers(0, 8))
+    # block 2: record #150 of the block becomes a zero record (ends the block)
+    in_b2 = np.flatnonzero(ref["file_offset"] // BLOCK_SIZE == 2)
+    if len(in_b2) > 150:
+        z = int(ref["file_offset"][in_b2[150]])
+        img[z:z + 7] = b"\0" * 7
+    # block 4: record #100 gets a length past the block end
+    in_b4 = np.flatnonzero(ref["file_offset"] // BLOCK_SIZE == 4)
+    if len(in_b4) > 100:
+        z = int(ref["file_offset"][in_b4[100]])
+        img[z + 4:z + 6] = (0xFFF0).to_bytes(2, "little")
+    img = bytes(img)
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    ref2 = oc.walk(img)
+    for v in VERIFY_VARIANTS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref2)
+    assert (ref2["status"] == 1).sum() > 10
+
+
 def test_verify_base_offset_and_random_bytes(gpu_ctx):
     rng = np.random.default_rng(14)
     img = rng.integers(0, 256, 5 * BLOCK_SIZE + 123, dtype=np.uint8).tobytes()  # garbage headers
