@@ -100,14 +100,16 @@ __global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint6
     }
 }
 
-// One wave copies len bytes src -> dst, any byte alignment of either: a byte
-// head up to dst's next 16-B boundary, then aligned 16-B stores whose source
-// bytes are funnel-shifted (v_alignbyte) out of 4-B-aligned dword loads (never
-// reading past the source range), then a byte tail.  Coalesced both ways.
-__device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
-    const uint32_t lane = lane_id();
+// G lanes (gl = 0..G-1 within the group) copy len bytes src -> dst, any byte
+// alignment of either: a byte head up to dst's next 16-B boundary, then
+// aligned 16-B stores whose source bytes are funnel-shifted (v_alignbyte) out
+// of 4-B-aligned dword loads (never reading past the source range), then a
+// byte tail.  Coalesced both ways.  G = 64: the whole wave.
+template <uint32_t G>
+__device__ __forceinline__ void group_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len,
+                                           uint32_t gl) {
     const uint32_t head = min(len, (16u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
-    if (lane < head) dst[lane] = src[lane];
+    for (uint32_t i = gl; i < head; i += G) dst[i] = src[i];
     const uint8_t* s = src + head;
     uint8_t* d = dst + head;
     const uint32_t n = len - head;
@@ -115,7 +117,7 @@ __device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ src, uint8
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s - sh);
     // vector v reads s4[4v .. 4v+3] (+ s4[4v+4] when sh != 0): stay inside [s, s+n)
     const uint32_t nvec = sh == 0 ? n / 16u : (n + sh >= 20u ? (n + sh - 20u) / 16u + 1u : 0u);
-    for (uint32_t v = lane; v < nvec; v += 64) {
+    for (uint32_t v = gl; v < nvec; v += G) {
         const uint32_t* q = s4 + 4u * v;
         const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = sh ? q[4] : 0u;
         uint4 o;
@@ -125,20 +127,41 @@ __device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ src, uint8
         o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
         *reinterpret_cast<uint4*>(d + 16u * v) = o;
     }
-    for (uint32_t i = nvec * 16u + lane; i < n; i += 64) d[i] = s[i];
+    for (uint32_t i = nvec * 16u + gl; i < n; i += G) d[i] = s[i];
 }
 
-// One wave per physical record that belongs to an emitted logical record.
+// Fragments of emitted logical records, 8 per wave visit: a fragment of at
+// most kSmallFrag bytes is copied by its own 8-lane group (small-record logs:
+// one wave per 131-B fragment left 7/8 of the wave and most of the visit idle),
+// larger ones then one after another by the whole wave.
+constexpr uint32_t kSmallFrag = 1024;
 __global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image_base,
                                const revel_record_result* __restrict__ phys, uint64_t n,
                                const uint64_t* __restrict__ frag_dst, uint8_t* __restrict__ payload) {
+    const uint32_t lane = lane_id(), grp = lane >> 3, gl = lane & 7u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint64_t k = w0; k < n; k += waves) {
-        const uint64_t dst = frag_dst[k];
-        if (dst == ~0ull) continue;
-        const revel_record_result r = phys[k];
-        wave_copy(image + (r.file_offset - image_base) + kHeaderSize, payload + dst, r.length);
+    for (uint64_t base = w0 * 8; base < n; base += waves * 8) {
+        const uint64_t k = base + grp;
+        const uint64_t dst = k < n ? frag_dst[k] : ~0ull;
+        uint64_t src_off = 0;
+        uint32_t len = 0;
+        if (dst != ~0ull) {
+            const revel_record_result r = phys[k];
+            src_off = r.file_offset - image_base + kHeaderSize;
+            len = r.length;
+        }
+        const bool small = dst != ~0ull && len <= kSmallFrag;
+        if (small) group_copy<8>(image + src_off, payload + dst, len, gl);
+        // large fragments: one bit per group (its lane 0), whole wave each
+        uint64_t big = __ballot(dst != ~0ull && !small && gl == 0);
+        while (big) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(big);
+            big &= big - 1;
+            const uint64_t so = __shfl(src_off, l, 64), dd = __shfl(dst, l, 64);
+            const uint32_t ln = __shfl(len, l, 64);
+            group_copy<64>(image + so, payload + dd, ln, lane);
+        }
     }
 }
 
@@ -165,7 +188,7 @@ hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, u
 hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
                         const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
                         hipStream_t st) {
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 3) / 4));
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 31) / 32));
     hipLaunchKernelGGL(k_reasm_gather, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<const uint8_t*>(d_image),
                        image_base, d_phys, n, d_frag_dst, static_cast<uint8_t*>(d_payload));
     return hipGetLastError();

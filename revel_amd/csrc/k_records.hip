@@ -432,12 +432,20 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
         bool have_round0 = true;
         // header list from the count pass (parallel per-block walks) when it
         // covers the whole block; otherwise lane 0 walks here.
-        const uint32_t nlist = (hlist && counts) ? counts[b] : kNone;
+        // lists (count pass + k_list_overflow) exist only for images starting on a block
+        const uint32_t nlist = (hlist && counts && lo_b == 0) ? counts[b] : kNone;
+        const uint32_t first_b = out_base;
+        uint32_t lpass = 0, lpass_off = 0;  // list batches of kListPerBlock records
+        uint64_t ent = (nlist != kNone && lane < nlist) ? hlist[b * kListStride + lane] : 0ull;
         for (;;) {
-            if (walk_from == lo_b && nlist <= kListPerBlock) {
-                const Hdr h = list_header(lane < nlist ? hlist[b * kListStride + lane] : 0ull);
-                const uint32_t off = lo_b + wave_exclusive_sum(lane < nlist ? kHeaderSize + h.len : 0u);
-                if (lane < nlist) {
+            const bool from_list = nlist != kNone;
+            if (from_list) {
+                const uint32_t k0 = lpass * kListPerBlock;
+                const uint32_t np = min(nlist - k0, kListPerBlock);
+                const Hdr h = list_header(ent);
+                const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
+                const uint32_t off = lpass_off + wave_exclusive_sum(sz);
+                if (lane < np) {
                     const bool bad = classify(h, off, bl) != REVEL_REC_OK;
                     wl.off[lane] = (uint16_t)off;
                     wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
@@ -445,10 +453,11 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
                     wl.acc[lane] = 0;
                 }
                 if (lane == 0) {
-                    wl.s[nlist] = wl.em1[nlist] = kNoRange;
-                    wl.nrec = nlist;
-                    wl.more_off = kNone;
+                    wl.s[np] = wl.em1[np] = kNoRange;
+                    wl.nrec = np;
+                    wl.more_off = k0 + np < nlist ? 1u : kNone;
                 }
+                lpass_off = __builtin_amdgcn_readlane(off + sz, np - 1u);
             } else if (lane == 0) {
                 uint32_t off = walk_from, n = 0, cont = kNone;
                 while (bl - off >= kHeaderSize) {
@@ -596,7 +605,15 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
             out_base += nrec;
             wave_lds_sync();
             if (cont == kNone) break;
-            walk_from = cont;
+            if (from_list) {
+                ++lpass;
+                if constexpr (!FRAME) {
+                    const uint32_t k0 = lpass * kListPerBlock;
+                    ent = k0 + lane < nlist ? *reinterpret_cast<const uint64_t*>(out + first_b + k0 + lane) : 0ull;
+                }
+            } else {
+                walk_from = cont;
+            }
         }
     }
 }
@@ -665,19 +682,29 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
         const uint32_t first_b = __builtin_amdgcn_readfirstlane(pf_first);
         uint32_t out_base = pf_first;
         uint32_t walk_from = 0;              // header walk (no list given)
-        uint32_t lpass = 0, lpass_off = 0;   // list passes: records [64 lpass, +64), first header offset
+        uint32_t lpass = 0, lpass_off = 0;   // list batches: records [128 lpass, +128), first header offset
         bool have_round0 = true;
         for (;;) {
             const bool from_list = use_list;
             if (from_list) {
                 // headers come from the count pass (the first kListPerBlock) or
                 // from k_list_overflow (the rest, in this block's result slots);
-                // offsets by prefix sum; the finalizer reads them back from LDS
-                const uint32_t k0 = lpass * kListPerBlock;
-                const uint32_t np = min(nlist - k0, kListPerBlock);
-                const Hdr h = list_header(ent);
+                // offsets by prefix sum; a batch is 128 records, two per lane
+                // (entries lane and lane + 64); the finalizer reads the first
+                // 64 headers back from LDS, the rest from the block
+                const uint32_t k0 = lpass * kRecCap2;
+                const uint32_t np = min(nlist - k0, kRecCap2);
+                uint64_t ent_b = 0;
+                if constexpr (!FRAME) {
+                    if (np > 64u && k0 + 64u + lane < nlist)
+                        ent_b = *reinterpret_cast<const uint64_t*>(out + first_b + k0 + 64u + lane);
+                }
+                const Hdr h = list_header(ent), hb = list_header(ent_b);
                 const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
-                const uint32_t off = lpass_off + wave_exclusive_sum(sz);
+                const uint32_t szb = lane + 64u < np ? kHeaderSize + hb.len : 0u;
+                const uint32_t exa = wave_exclusive_sum(sz);
+                const uint32_t off = lpass_off + exa;
+                const uint32_t offb = lpass_off + __builtin_amdgcn_readlane(exa + sz, 63) + wave_exclusive_sum(szb);
                 if (lane < np) {
                     const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
                     wl.off[lane] = (uint16_t)off;
@@ -687,12 +714,21 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                     wl.hstored[lane] = h.stored;
                     wl.hlt[lane] = h.len | (h.type << 16);
                 }
+                if (lane + 64u < np) {
+                    const bool bad = classify(hb, offb, kBlockSize) != REVEL_REC_OK;
+                    wl.off[lane + 64u] = (uint16_t)offb;
+                    wl.s[lane + 64u] = bad ? kNoRange : (uint16_t)(offb + 6);
+                    wl.em1[lane + 64u] = bad ? kNoRange : (uint16_t)(offb + kHeaderSize + hb.len - 1u);
+                    wl.acc[lane + 64u] = 0;
+                }
                 if (lane == 0) {
                     wl.s[np] = wl.em1[np] = kNoRange;
                     wl.nrec = np;
                     wl.more_off = k0 + np < nlist ? 1u : kNone;
                 }
-                lpass_off = __builtin_amdgcn_readlane(off + sz, np - 1u);  // header offset of the next pass
+                // header offset of the next batch
+                lpass_off = np > 64u ? __builtin_amdgcn_readlane(offb + szb, np - 65u)
+                                     : __builtin_amdgcn_readlane(off + sz, np - 1u);
             } else if (lane == 0) {
                 uint32_t off = walk_from, n = 0, cont = kNone;
                 while (kBlockSize - off >= kHeaderSize) {
@@ -830,7 +866,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             if (from_list) {
                 ++lpass;
                 if constexpr (!FRAME) {
-                    const uint32_t k0 = lpass * kListPerBlock;
+                    const uint32_t k0 = lpass * kRecCap2;
                     ent = k0 + lane < nlist ? *reinterpret_cast<const uint64_t*>(out + first_b + k0 + lane) : 0ull;
                 }
             } else {
@@ -964,15 +1000,6 @@ template <bool FRAME>
 static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                  uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
-    if (!FRAME && hl && d_counts) {
-        // list the headers of blocks with more than kListPerBlock records
-        const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
-        hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
-                           d_out);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
     hipLaunchKernelGGL((k_verify_records3<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
                        base_offset, d_first, d_out, lead, hl, d_counts);
     hipError_t e = hipGetLastError();
@@ -1015,6 +1042,14 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     const uint64_t* hl = variant == 2 ? nullptr : d_hlist;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    if (hl && d_counts) {
+        // list the headers of blocks with more than kListPerBlock records
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
+        hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
+                           d_out);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     const bool partial = nbytes % kBlockSize != 0;
     switch (variant) {
         case 3: return launch_verify2<false, BP_MASK>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
