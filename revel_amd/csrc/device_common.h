@@ -382,4 +382,34 @@ __device__ __forceinline__ uint32_t wave_exclusive_sum(uint32_t v) {
     return incl - v;
 }
 
+// G lanes (gl = 0..G-1 within the group) copy len bytes src -> dst, any byte
+// alignment of either: a byte head up to dst's next 16-B boundary, then
+// aligned 16-B stores whose source bytes are funnel-shifted (v_alignbyte) out
+// of 4-B-aligned dword loads (never reading past the source range), then a
+// byte tail.  Coalesced both ways.  G = 64: the whole wave.
+template <uint32_t G>
+__device__ __forceinline__ void group_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len,
+                                           uint32_t gl) {
+    const uint32_t head = min(len, (16u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
+    for (uint32_t i = gl; i < head; i += G) dst[i] = src[i];
+    const uint8_t* s = src + head;
+    uint8_t* d = dst + head;
+    const uint32_t n = len - head;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s - sh);
+    // vector v reads s4[4v .. 4v+3] (+ s4[4v+4] when sh != 0): stay inside [s, s+n)
+    const uint32_t nvec = sh == 0 ? n / 16u : (n + sh >= 20u ? (n + sh - 20u) / 16u + 1u : 0u);
+    for (uint32_t v = gl; v < nvec; v += G) {
+        const uint32_t* q = s4 + 4u * v;
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = sh ? q[4] : 0u;
+        uint4 o;
+        o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        *reinterpret_cast<uint4*>(d + 16u * v) = o;
+    }
+    for (uint32_t i = nvec * 16u + gl; i < n; i += G) d[i] = s[i];
+}
+
 }  // namespace

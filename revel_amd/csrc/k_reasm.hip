@@ -100,36 +100,6 @@ __global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint6
     }
 }
 
-// G lanes (gl = 0..G-1 within the group) copy len bytes src -> dst, any byte
-// alignment of either: a byte head up to dst's next 16-B boundary, then
-// aligned 16-B stores whose source bytes are funnel-shifted (v_alignbyte) out
-// of 4-B-aligned dword loads (never reading past the source range), then a
-// byte tail.  Coalesced both ways.  G = 64: the whole wave.
-template <uint32_t G>
-__device__ __forceinline__ void group_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len,
-                                           uint32_t gl) {
-    const uint32_t head = min(len, (16u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
-    for (uint32_t i = gl; i < head; i += G) dst[i] = src[i];
-    const uint8_t* s = src + head;
-    uint8_t* d = dst + head;
-    const uint32_t n = len - head;
-    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3u);
-    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s - sh);
-    // vector v reads s4[4v .. 4v+3] (+ s4[4v+4] when sh != 0): stay inside [s, s+n)
-    const uint32_t nvec = sh == 0 ? n / 16u : (n + sh >= 20u ? (n + sh - 20u) / 16u + 1u : 0u);
-    for (uint32_t v = gl; v < nvec; v += G) {
-        const uint32_t* q = s4 + 4u * v;
-        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = sh ? q[4] : 0u;
-        uint4 o;
-        o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
-        o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
-        *reinterpret_cast<uint4*>(d + 16u * v) = o;
-    }
-    for (uint32_t i = nvec * 16u + gl; i < n; i += G) d[i] = s[i];
-}
-
 // Fragments of emitted logical records, 8 per wave visit: a fragment of at
 // most kSmallFrag bytes is copied by its own 8-lane group (small-record logs:
 // one wave per 131-B fragment left 7/8 of the wave and most of the visit idle),
@@ -141,15 +111,24 @@ __global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image
     const uint32_t lane = lane_id(), grp = lane >> 3, gl = lane & 7u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // descriptors one visit ahead: the next visit's loads are in flight while
+    // this visit copies
+    uint64_t dst_n = w0 * 8 + grp < n ? frag_dst[w0 * 8 + grp] : ~0ull;
+    uint64_t off_n = 0;
+    uint32_t len_n = 0;
+    if (w0 * 8 + grp < n) {
+        off_n = phys[w0 * 8 + grp].file_offset;
+        len_n = phys[w0 * 8 + grp].length;
+    }
     for (uint64_t base = w0 * 8; base < n; base += waves * 8) {
-        const uint64_t k = base + grp;
-        const uint64_t dst = k < n ? frag_dst[k] : ~0ull;
-        uint64_t src_off = 0;
-        uint32_t len = 0;
-        if (dst != ~0ull) {
-            const revel_record_result r = phys[k];
-            src_off = r.file_offset - image_base + kHeaderSize;
-            len = r.length;
+        const uint64_t dst = dst_n;
+        const uint64_t src_off = off_n - image_base + kHeaderSize;
+        const uint32_t len = len_n;
+        const uint64_t kn = base + waves * 8 + grp;
+        dst_n = kn < n ? frag_dst[kn] : ~0ull;
+        if (kn < n) {
+            off_n = phys[kn].file_offset;
+            len_n = phys[kn].length;
         }
         const bool small = dst != ~0ull && len <= kSmallFrag;
         if (small) group_copy<8>(image + src_off, payload + dst, len, gl);

@@ -884,25 +884,40 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 // ---------------------------------------------------------------------------
 __global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const revel::FragDesc* __restrict__ frags,
                                     uint64_t nfrags, uint8_t* __restrict__ image) {
+    // 8 fragments per wave visit: one of at most kSmallFragment payload bytes
+    // (or a trailer) is written by its own 8-lane group, larger ones then by
+    // the whole wave (group_copy: aligned 16-B stores)
+    constexpr uint32_t kSmallFragment = 1024;
+    const uint32_t lane = lane_id(), grp = lane >> 3, gl = lane & 7u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t f = blockIdx.x * (uint64_t)(blockDim.x / 64) + (threadIdx.x >> 6); f < nfrags; f += waves) {
-        const revel::FragDesc d = frags[f];
+    const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // descriptors one visit ahead: the next visit's load is in flight while
+    // this visit copies
+    revel::FragDesc dn{0, 0, 0, revel::kTrailer};
+    if (w0 * 8 + grp < nfrags) dn = frags[w0 * 8 + grp];
+    for (uint64_t base = w0 * 8; base < nfrags; base += waves * 8) {
+        const uint64_t f = base + grp;
+        const revel::FragDesc d = dn;
+        if (base + waves * 8 + grp < nfrags) dn = frags[base + waves * 8 + grp];
         uint8_t* dst = image + d.dst;
-        const uint32_t lane = lane_id();
-        if (d.type == revel::kTrailer) {
-            for (uint32_t i = lane; i < d.len; i += 64) dst[i] = 0;
-            continue;
+        if (f < nfrags) {
+            if (d.type == revel::kTrailer) {
+                if (gl < d.len) dst[gl] = 0;  // a trailer is < 7 bytes
+            } else if (gl < kHeaderSize) {
+                const uint32_t hv = gl < 4 ? 0u : gl == 4 ? (d.len & 0xffu) : gl == 5 ? (d.len >> 8) : d.type;
+                dst[gl] = (uint8_t)hv;
+            }
         }
-        if (lane < 7) {
-            const uint8_t hv[7] = {0, 0, 0, 0, (uint8_t)(d.len & 0xffu), (uint8_t)(d.len >> 8), (uint8_t)d.type};
-            dst[lane] = hv[lane];
-        }
-        const uint8_t* src = payloads + d.src;
-        uint8_t* pd = dst + kHeaderSize;
-        for (uint32_t i = lane * 4; i < d.len; i += 256) {
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-                if (i + k < d.len) pd[i + k] = src[i + k];
+        const bool payload = f < nfrags && d.type != revel::kTrailer;
+        const bool small = payload && d.len <= kSmallFragment;
+        if (small) group_copy<8>(payloads + d.src, dst + kHeaderSize, d.len, gl);
+        uint64_t big = __ballot(payload && !small && gl == 0);
+        while (big) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(big);
+            big &= big - 1;
+            const uint64_t so = __shfl(d.src, l, 64), dd = __shfl(d.dst, l, 64);
+            const uint32_t ln = __shfl(d.len, l, 64);
+            group_copy<64>(payloads + so, image + dd + kHeaderSize, ln, lane);
         }
     }
 }
@@ -1093,7 +1108,7 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
                          void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st) {
     if (nfrags) {
-        const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (nfrags + 3) / 4));
+        const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (nfrags + 31) / 32));
         hipLaunchKernelGGL(k_scatter_fragments, dim3((uint32_t)grid), dim3(256), 0, st,
                            static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image));
         hipError_t e = hipGetLastError();
