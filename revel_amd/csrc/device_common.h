@@ -202,8 +202,32 @@ __device__ __forceinline__ uint32_t absorb(uint32_t crc, uint32_t w, LaneConst L
     }
 }
 
+// x-state form of an S4R step: the chain carries x = crc ^ (next word), so
+// the four table words and the following data word fold with two 3-input
+// xors (v_bitop3_b32, truth table 0x96) instead of four v_xor_b32.  wn = the
+// stream's next word (0 after the last one: then the result is the crc).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t step_x(uint32_t x, uint32_t wn, LaneConst L, const uint32_t* tab) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, L.lc1, Sel<2>::v);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, L.lc1, Sel<3>::v);
+    return xor3(xor3(ldsw<0>(tab, a0), ldsw<128>(tab, a1), ldsw<0>(tab, a2)), ldsw<128>(tab, a3), wn);
+}
+
 template <int TM>
 __device__ __forceinline__ uint32_t absorb4(uint32_t crc, uint4 v, LaneConst L, const uint32_t* tab) {
+    if constexpr (TM == TM_S4R) {
+        // x-state chain over the four words: 1 xor + 7 three-input xors
+        // instead of 16 two-input ones
+        uint32_t x = crc ^ v.x;
+        x = step_x(x, v.y, L, tab);
+        x = step_x(x, v.z, L, tab);
+        x = step_x(x, v.w, L, tab);
+        return step_x(x, 0u, L, tab);
+    }
     crc = absorb<TM>(crc, v.x, L, tab);
     crc = absorb<TM>(crc, v.y, L, tab);
     crc = absorb<TM>(crc, v.z, L, tab);

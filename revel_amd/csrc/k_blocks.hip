@@ -321,7 +321,7 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     return NT ? ldg4(reinterpret_cast<const uint4*>(p)) : ldg4_plain(reinterpret_cast<const uint4*>(p));
 }
 
-template <int THREADS, bool NT, bool FRAME>
+template <int THREADS, bool NT, bool FRAME, bool XS = false>
 __global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                           uint32_t* __restrict__ masked_out,
                                                           uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
@@ -359,13 +359,30 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restr
                 load_round(nxt, b + nwaves, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (r == 0) zero_header_bytes(cur[0], l0, FRAME, &hdr);
+            if (r == 0) {
+                zero_header_bytes(cur[0], l0, FRAME, &hdr);
+                if constexpr (XS) {
+                    u0 = cur[0].x; u1 = cur[0].y; u2 = cur[0].z; u3 = cur[0].w;
+                }
+            }
+            if constexpr (XS) {
+                // u = crc ^ (word k); fold word k + 1 (next round's first, or 0 at the end)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                u0 = absorb<TM_S4R>(u0, cur[k].x, L, tab);
-                u1 = absorb<TM_S4R>(u1, cur[k].y, L, tab);
-                u2 = absorb<TM_S4R>(u2, cur[k].z, L, tab);
-                u3 = absorb<TM_S4R>(u3, cur[k].w, L, tab);
+                for (int k = 0; k < 8; ++k) {
+                    const uint4 wn = k < 7 ? cur[k + 1] : (r < 3 ? nxt[0] : make_uint4(0, 0, 0, 0));
+                    u0 = step_x(u0, wn.x, L, tab);
+                    u1 = step_x(u1, wn.y, L, tab);
+                    u2 = step_x(u2, wn.z, L, tab);
+                    u3 = step_x(u3, wn.w, L, tab);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    u0 = absorb<TM_S4R>(u0, cur[k].x, L, tab);
+                    u1 = absorb<TM_S4R>(u1, cur[k].y, L, tab);
+                    u2 = absorb<TM_S4R>(u2, cur[k].z, L, tab);
+                    u3 = absorb<TM_S4R>(u3, cur[k].w, L, tab);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -410,10 +427,10 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restr
     }
 }
 
-template <int THREADS, bool NT, bool FRAME>
+template <int THREADS, bool NT, bool FRAME, bool XS = false>
 hipError_t launch_full3(const DeviceInfo& di, const uint8_t* blocks, uint64_t n, uint32_t* masked, uint8_t* ok,
                         uint8_t* frame_dst, hipStream_t st) {
-    auto kern = k_full_blocks3<THREADS, NT, FRAME>;
+    auto kern = k_full_blocks3<THREADS, NT, FRAME, XS>;
     const uint64_t wg_needed = (n + THREADS / 64 - 1) / (THREADS / 64);
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, wg_needed));
     hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked, ok, frame_dst);
@@ -440,8 +457,9 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
                                    uint32_t* d_masked, uint8_t* d_ok, hipStream_t st) {
     const uint8_t* b = static_cast<const uint8_t*>(d_blocks);
     switch (variant) {
-        // production: v3 interleaved word streams (gap-folded tables), nt loads
-        case 0: return launch_full3<1024, true, false>(di, b, n, d_masked, d_ok, nullptr, st);
+        // production: v3 interleaved word streams (gap-folded tables), nt loads,
+        // x-state chains (3-input xors)
+        case 0: return launch_full3<1024, true, false, true>(di, b, n, d_masked, d_ok, nullptr, st);
         case 9: return launch_full<TM_S4R, 1024, LM_DIRECT, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         case 8: return launch_full<TM_S2R, 768, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         // v2 (pipelined across blocks): chains x epilogue
@@ -453,6 +471,8 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
         // v3: interleaved word streams, gap folded into the tables
         case 20: return launch_full3<1024, true, false>(di, b, n, d_masked, d_ok, nullptr, st);
         case 21: return launch_full3<1024, false, false>(di, b, n, d_masked, d_ok, nullptr, st);
+        // v3 with the x-state chain (3-input xors) = production
+        case 22: return launch_full3<1024, true, false, true>(di, b, n, d_masked, d_ok, nullptr, st);
         case 1: return launch_full<TM_S2R, 512, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         case 2: return launch_full<TM_S4R, 256, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         case 3: return launch_full<TM_S4, 1024, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
@@ -471,7 +491,7 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
 
 hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st) {
     uint8_t* b = static_cast<uint8_t*>(d_blocks);
-    return launch_full3<1024, true, true>(di, b, n, nullptr, nullptr, b, st);
+    return launch_full3<1024, true, true, true>(di, b, n, nullptr, nullptr, b, st);
 }
 
 hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
