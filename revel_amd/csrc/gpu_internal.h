@@ -24,7 +24,7 @@ struct DeviceInfo {
     int num_cu = 256;
 };
 
-// variant: 0 = production (S2R, 512 threads, 2 WG/CU); others are the
+// variant: 0 = production (k_full_blocks4: interleaved word streams, load ring); others are the
 // experiment arms listed in k_blocks.hip (100 = streaming-read ceiling).
 hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void* d_blocks, uint64_t n,
                                    uint32_t* d_masked, uint8_t* d_ok, hipStream_t st);

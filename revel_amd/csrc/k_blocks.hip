@@ -58,7 +58,7 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks(const uint8_t* __restri
 
 // Read-only streaming ceiling with the same grid and block assignment:
 // coalesced 16 B/lane loads of the whole block, xor-folded, 4 B written.
-template <int THREADS>
+template <int THREADS, bool NT = true>
 __global__ __launch_bounds__(THREADS) void k_stream_ceiling(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                             uint32_t* __restrict__ out) {
     const uint64_t waves_per_wg = THREADS / 64;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(THREADS) void k_stream_ceiling(const uint8_t* __res
         uint4 acc = {0, 0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
-            uint4 v = ldg4(p + k * 64);
+            uint4 v = NT ? ldg4(p + k * 64) : ldg4_plain(p + k * 64);
             acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
         }
         uint32_t r = xor_reduce_wave(acc.x ^ acc.y ^ acc.z ^ acc.w);
@@ -321,6 +321,51 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     return NT ? ldg4(reinterpret_cast<const uint4*>(p)) : ldg4_plain(reinterpret_cast<const uint4*>(p));
 }
 
+// Block epilogue of the interleaved-stream kernels: R = XOR_s U_s x^(-32 s)
+// by the 8-level inverse-shift tree (2 levels in-lane, 6 across lanes), then
+// the masked CRC, the header check or the framed header.
+template <bool FRAME>
+__device__ __forceinline__ void finish_full_block(uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3, uint4 hdr,
+                                                  uint64_t b, const uint32_t* shtab, uint32_t lane,
+                                                  uint32_t* __restrict__ masked_out, uint8_t* __restrict__ ok_out,
+                                                  uint8_t* __restrict__ frame_dst) {
+    uint32_t v0 = u0 ^ tree_shift<0>(shtab, u1);
+    uint32_t v1 = u2 ^ tree_shift<0>(shtab, u3);
+    uint32_t v = v0 ^ tree_shift<1>(shtab, v1);
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        uint32_t t;
+        switch (lv) {
+            case 0: t = tree_shift<2>(shtab, v); break;
+            case 1: t = tree_shift<3>(shtab, v); break;
+            case 2: t = tree_shift<4>(shtab, v); break;
+            case 3: t = tree_shift<5>(shtab, v); break;
+            case 4: t = tree_shift<6>(shtab, v); break;
+            default: t = tree_shift<7>(shtab, v); break;
+        }
+        const uint32_t dn = __shfl_down(t, 1u << lv, 64);
+        const uint32_t m = (2u << lv) - 1u;
+        v = ((lane & m) == 0u) ? (v ^ dn) : v;
+    }
+    const uint32_t raw = __builtin_amdgcn_readfirstlane(v);
+    const uint32_t masked = mask(raw ^ kFullInitXor);
+    if (lane == 0) {
+        if constexpr (FRAME) {
+            uint2 h;
+            h.x = masked;
+            h.y = (hdr.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16) | kFullPayload;
+            *reinterpret_cast<uint2*>(frame_dst + b * kBlockSize) = h;
+        } else {
+            masked_out[b] = masked;
+            if (ok_out) {
+                const bool ok = (hdr.x == masked) && ((hdr.y & 0xFFFFu) == kFullPayload) &&
+                                (((hdr.y >> 16) & 0xFFu) == kFullTypeByte);
+                ok_out[b] = ok ? 1 : 0;
+            }
+        }
+    }
+}
+
 template <int THREADS, bool NT, bool FRAME, bool XS = false>
 __global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                           uint32_t* __restrict__ masked_out,
@@ -388,42 +433,7 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restr
 #pragma unroll
             for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
         }
-        // ---- tree combine: R = XOR_s U_s x^(-32 s) ----
-        uint32_t v0 = u0 ^ tree_shift<0>(shtab, u1);
-        uint32_t v1 = u2 ^ tree_shift<0>(shtab, u3);
-        uint32_t v = v0 ^ tree_shift<1>(shtab, v1);
-#pragma unroll
-        for (int lv = 0; lv < 6; ++lv) {
-            uint32_t t;
-            switch (lv) {
-                case 0: t = tree_shift<2>(shtab, v); break;
-                case 1: t = tree_shift<3>(shtab, v); break;
-                case 2: t = tree_shift<4>(shtab, v); break;
-                case 3: t = tree_shift<5>(shtab, v); break;
-                case 4: t = tree_shift<6>(shtab, v); break;
-                default: t = tree_shift<7>(shtab, v); break;
-            }
-            const uint32_t dn = __shfl_down(t, 1u << lv, 64);
-            const uint32_t m = (2u << lv) - 1u;
-            v = ((lane & m) == 0u) ? (v ^ dn) : v;
-        }
-        const uint32_t raw = __builtin_amdgcn_readfirstlane(v);
-        const uint32_t masked = mask(raw ^ kFullInitXor);
-        if (l0) {
-            if constexpr (FRAME) {
-                uint2 h;
-                h.x = masked;
-                h.y = (hdr.y & 0xFF000000u) | (uint32_t(kFullTypeByte) << 16) | kFullPayload;
-                *reinterpret_cast<uint2*>(frame_dst + b * kBlockSize) = h;
-            } else {
-                masked_out[b] = masked;
-                if (ok_out) {
-                    const bool ok = (hdr.x == masked) && ((hdr.y & 0xFFFFu) == kFullPayload) &&
-                                    (((hdr.y >> 16) & 0xFFu) == kFullTypeByte);
-                    ok_out[b] = ok ? 1 : 0;
-                }
-            }
-        }
+        finish_full_block<FRAME>(u0, u1, u2, u3, hdr, b, shtab, lane, masked_out, ok_out, frame_dst);
     }
 }
 
@@ -434,6 +444,74 @@ hipError_t launch_full3(const DeviceInfo& di, const uint8_t* blocks, uint64_t n,
     const uint64_t wg_needed = (n + THREADS / 64 - 1) / (THREADS / 64);
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, wg_needed));
     hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked, ok, frame_dst);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Config C2, v4: v3's streams and x-state chains fed by a 16-slot load ring.
+// Row g of a block (g = 0..31) is the 1 KiB [1024 g, +1024), 16 B per lane.
+// v3 double-buffers whole 8 KiB rounds (cur / nxt), so while a round is folded
+// only the next one is in flight.  Here the slot a row leaves is refilled at
+// once with the row 16 ahead (into the next block at the end), so ~15 rows =
+// 15 KiB per wave stay in flight with the same 64 VGPRs: HBM sees ~2x the
+// bytes in flight per CU.  All loads are unconditional (rows past the last
+// block re-read the last block), so the compiler's vmcnt counts stay exact.
+// ---------------------------------------------------------------------------
+template <int THREADS, bool FRAME>
+__global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restrict__ blocks, uint64_t nblocks,
+                                                          uint32_t* __restrict__ masked_out,
+                                                          uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
+    __shared__ uint32_t tab[32768];      // 128 KiB: T'' replicated 32x
+    __shared__ uint32_t shtab[8 * 1024];  // 32 KiB: inverse-shift tree tables
+    fill_gap_tables(tab);
+    fill_inv_tree_tables(shtab);
+    __syncthreads();
+    const LaneConst L = make_lane_const();
+    const uint32_t lane = lane_id();
+    const bool l0 = lane == 0;
+    const uint64_t waves_per_wg = THREADS / 64;
+    const uint64_t gwave = blockIdx.x * waves_per_wg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    if (gwave >= nblocks) return;
+    const uint8_t* lane_base = blocks + lane * 16u;
+    auto row = [&](uint64_t b, int g) {
+        b = b < nblocks ? b : nblocks - 1;
+        return ldg4(reinterpret_cast<const uint4*>(lane_base + b * kBlockSize + g * 1024));
+    };
+    uint4 ring[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) ring[g] = row(gwave, g);
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+        uint32_t u0, u1, u2, u3;
+        uint4 hdr;
+#pragma unroll
+        for (int g = 0; g < 32; ++g) {
+            if (g == 0) {
+                uint4 c = ring[0];
+                zero_header_bytes(c, l0, FRAME, &hdr);
+                u0 = c.x; u1 = c.y; u2 = c.z; u3 = c.w;
+                ring[0] = row(b, 16);
+            }
+            // fold row g + 1 (0 after the last row): u = crc ^ (word g + 1)
+            const uint4 wn = g < 31 ? ring[(g + 1) & 15] : make_uint4(0, 0, 0, 0);
+            u0 = step_x(u0, wn.x, L, tab);
+            u1 = step_x(u1, wn.y, L, tab);
+            u2 = step_x(u2, wn.z, L, tab);
+            u3 = step_x(u3, wn.w, L, tab);
+            // row g + 1 has left its slot: refill with row g + 17
+            if (g < 31) ring[(g + 1) & 15] = g + 17 < 32 ? row(b, g + 17) : row(b + nwaves, g + 17 - 32);
+        }
+        finish_full_block<FRAME>(u0, u1, u2, u3, hdr, b, shtab, lane, masked_out, ok_out, frame_dst);
+    }
+}
+
+template <int THREADS, bool FRAME>
+hipError_t launch_full4(const DeviceInfo& di, const uint8_t* blocks, uint64_t n, uint32_t* masked, uint8_t* ok,
+                        uint8_t* frame_dst, hipStream_t st) {
+    const uint64_t wg_needed = (n + THREADS / 64 - 1) / (THREADS / 64);
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, wg_needed));
+    hipLaunchKernelGGL((k_full_blocks4<THREADS, FRAME>), dim3((uint32_t)grid), dim3(THREADS), 0, st, blocks, n, masked,
+                       ok, frame_dst);
     return hipGetLastError();
 }
 
@@ -449,6 +527,15 @@ hipError_t launch_full(const DeviceInfo& di, int wg_per_cu, const uint8_t* block
     return hipGetLastError();
 }
 
+template <int THREADS, bool NT>
+hipError_t launch_stream(const DeviceInfo& di, int wg_per_cu, const uint8_t* b, uint64_t n, uint32_t* out,
+                         hipStream_t st) {
+    const uint64_t w = THREADS / 64;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * wg_per_cu, (n + w - 1) / w));
+    hipLaunchKernelGGL((k_stream_ceiling<THREADS, NT>), dim3((uint32_t)grid), dim3(THREADS), 0, st, b, n, out);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 namespace revel {
@@ -457,9 +544,9 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
                                    uint32_t* d_masked, uint8_t* d_ok, hipStream_t st) {
     const uint8_t* b = static_cast<const uint8_t*>(d_blocks);
     switch (variant) {
-        // production: v3 interleaved word streams (gap-folded tables), nt loads,
-        // x-state chains (3-input xors)
-        case 0: return launch_full3<1024, true, false, true>(di, b, n, d_masked, d_ok, nullptr, st);
+        // production: v4 = v3 interleaved word streams (gap-folded tables, nt
+        // loads) with x-state chains (3-input xors), fed by a 16-slot load ring
+        case 0: return launch_full4<1024, false>(di, b, n, d_masked, d_ok, nullptr, st);
         case 9: return launch_full<TM_S4R, 1024, LM_DIRECT, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         case 8: return launch_full<TM_S2R, 768, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         // v2 (pipelined across blocks): chains x epilogue
@@ -471,8 +558,10 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
         // v3: interleaved word streams, gap folded into the tables
         case 20: return launch_full3<1024, true, false>(di, b, n, d_masked, d_ok, nullptr, st);
         case 21: return launch_full3<1024, false, false>(di, b, n, d_masked, d_ok, nullptr, st);
-        // v3 with the x-state chain (3-input xors) = production
+        // v3 with the x-state chain (3-input xors)
         case 22: return launch_full3<1024, true, false, true>(di, b, n, d_masked, d_ok, nullptr, st);
+        // v4: v3 + x-state fed by a 16-slot load ring (~15 KiB in flight per wave) = production
+        case 23: return launch_full4<1024, false>(di, b, n, d_masked, d_ok, nullptr, st);
         case 1: return launch_full<TM_S2R, 512, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         case 2: return launch_full<TM_S4R, 256, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
         case 3: return launch_full<TM_S4, 1024, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st);
@@ -485,13 +574,20 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
             hipLaunchKernelGGL(k_stream_ceiling<256>, dim3((uint32_t)grid), dim3(256), 0, st, b, n, d_masked);
             return hipGetLastError();
         }
+        // streaming-read ceiling shapes (experiment): plain loads; fewer / more waves per CU
+        case 101: return launch_stream<256, false>(di, 8, b, n, d_masked, st);
+        case 102: return launch_stream<256, true>(di, 4, b, n, d_masked, st);
+        case 103: return launch_stream<256, true>(di, 2, b, n, d_masked, st);
+        case 104: return launch_stream<1024, true>(di, 1, b, n, d_masked, st);
+        case 105: return launch_stream<512, true>(di, 4, b, n, d_masked, st);
+        case 106: return launch_stream<256, true>(di, 16, b, n, d_masked, st);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st) {
     uint8_t* b = static_cast<uint8_t*>(d_blocks);
-    return launch_full3<1024, true, true, true>(di, b, n, nullptr, nullptr, b, st);
+    return launch_full4<1024, true>(di, b, n, nullptr, nullptr, b, st);
 }
 
 hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,

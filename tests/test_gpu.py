@@ -15,7 +15,7 @@ from oracle import oracle_c as oc
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 20, 21, 22]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 20, 21, 22, 23]
 
 
 def run_full(ctx, host_blocks, variant=None):
