@@ -171,7 +171,12 @@ int revel_gpu_frame_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t n
  * (d_counts[nblocks]); (2) walk + CRC every record, writing record k of
  * block b to d_out[d_first[b] + k] where d_first is the exclusive prefix sum
  * of d_counts (revel_gpu_exclusive_scan_u32 computes it on device).
- * nbytes need not be a block multiple (the last block may be partial). */
+ * nbytes need not be a block multiple (the last block may be partial).
+ * The count pass also leaves per-block header lists in the context: a verify
+ * of the same image on the same context uses them (for blocks with more than
+ * 64 records it first lists the rest into their own d_out slots, which it
+ * then overwrites with the results); without them verify walks the headers
+ * itself, with the same results, slower. */
 int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,
                             uint32_t* d_counts, void* stream);
 int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, uint32_t* d_out,
