@@ -71,8 +71,15 @@ hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_
 hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t nblocks, uint64_t base_offset,
                             uint64_t* d_summary, hipStream_t st);
 
+// d_counts / d_first / d_xlist (all or none): per virtual block (image byte 0
+// at in-block offset lead) the number of records and the fragment index of
+// its first record, and one u64 header-list entry per fragment (written by
+// the scatter); with them the CRC pass reads its header lists instead of
+// walking the headers of every block.
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
-                         void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st);
+                         void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st,
+                         const uint32_t* d_counts = nullptr, const uint32_t* d_first = nullptr,
+                         uint64_t* d_xlist = nullptr);
 
 hipError_t batch_count(const DeviceInfo& di, const void* d_payload, uint64_t payload_bytes,
                        const revel_logical_record* d_logical, uint64_t n, revel_batch_info* d_info, uint64_t* d_nent,

@@ -397,16 +397,42 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
     if (len && (!d_image || (!d_payloads && frags.size()))) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    // Header lists for the device CRC pass: per virtual block (image byte 0 at
+    // in-block offset `lead`) its record count and the fragment index of its
+    // first record; the scatter kernel writes one entry per fragment.
+    const uint64_t vblocks = (len + lead + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
+    std::vector<uint32_t> counts, first;
+    const bool lists = !frags.empty() && frags.size() < (1ull << 32);
+    if (lists) {
+        counts.assign(vblocks, 0);
+        first.assign(vblocks, 0);
+        for (size_t f = 0; f < frags.size(); ++f) {
+            if (frags[f].type == revel::kTrailer) continue;
+            const uint64_t vb = (frags[f].dst + lead) / REVEL_BLOCK_SIZE;
+            if (counts[vb]++ == 0) first[vb] = (uint32_t)f;
+        }
+    }
+    revel::DeviceScratch scratch;
     revel::FragDesc* d_frags = nullptr;
+    uint32_t *d_counts = nullptr, *d_first = nullptr;
+    uint64_t* d_xlist = nullptr;
     hipError_t e = hipSuccess;
     if (!frags.empty()) {
-        e = hipMalloc(reinterpret_cast<void**>(&d_frags), frags.size() * sizeof(revel::FragDesc));
+        e = scratch.get(&d_frags, frags.size());
         if (e == hipSuccess)
             e = hipMemcpyAsync(d_frags, frags.data(), frags.size() * sizeof(revel::FragDesc), hipMemcpyHostToDevice, st);
     }
-    if (e == hipSuccess) e = revel::frame_records(ctx->di, d_payloads, d_frags, frags.size(), d_image, len, lead, st);
+    if (lists) {
+        if (e == hipSuccess) e = scratch.get(&d_counts, vblocks);
+        if (e == hipSuccess) e = scratch.get(&d_first, vblocks);
+        if (e == hipSuccess) e = scratch.get(&d_xlist, frags.size());
+        if (e == hipSuccess) e = hipMemcpyAsync(d_counts, counts.data(), vblocks * 4, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_first, first.data(), vblocks * 4, hipMemcpyHostToDevice, st);
+    }
+    if (e == hipSuccess)
+        e = revel::frame_records(ctx->di, d_payloads, d_frags, frags.size(), d_image, len, lead, st, d_counts, d_first,
+                                 d_xlist);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (d_frags) (void)hipFree(d_frags);
     if (e != hipSuccess) return set_error(REVEL_IO_ERROR, "append_records: %s", hipGetErrorString(e));
     *image_len = len;
     *block_offset = boff;

@@ -387,7 +387,9 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
                                                                      revel_record_result* __restrict__ out,
                                                                      uint32_t lead,
                                                                      const uint64_t* __restrict__ hlist,
-                                                                     const uint32_t* __restrict__ counts) {
+                                                                     const uint32_t* __restrict__ counts,
+                                                                     const uint64_t* __restrict__ xlist = nullptr,
+                                                                     uint32_t xstride = 3) {
     __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
     __shared__ VerifyWaveLds2 wl_all[THREADS / 64];
     fill_tables<TM>(tab);
@@ -432,11 +434,16 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
         bool have_round0 = true;
         // header list from the count pass (parallel per-block walks) when it
         // covers the whole block; otherwise lane 0 walks here.
-        // lists (count pass + k_list_overflow) exist only for images starting on a block
-        const uint32_t nlist = (hlist && counts && lo_b == 0) ? counts[b] : kNone;
-        const uint32_t first_b = out_base;
-        uint32_t lpass = 0, lpass_off = 0;  // list batches of kListPerBlock records
-        uint64_t ent = (nlist != kNone && lane < nlist) ? hlist[b * kListStride + lane] : 0ull;
+        // header lists: verify = the count pass's (records 0..63 in hlist, the rest
+        // in the result slots, xlist = out, stride 3), only for images starting on
+        // a block; FRAME = entry k of block b at xlist[first[b] + k], any lead
+        const bool have_list = FRAME ? (counts && first && xlist) : (hlist && counts && xlist && lo_b == 0);
+        const uint32_t nlist = have_list ? counts[b] : kNone;
+        const uint32_t first_b = FRAME ? (have_list ? first[b] : 0u) : out_base;
+        uint32_t lpass = 0, lpass_off = lo_b;  // list batches of kListPerBlock records
+        uint64_t ent = 0;
+        if (nlist != kNone && lane < nlist)
+            ent = FRAME ? xlist[uint64_t(first_b) + lane] : hlist[b * kListStride + lane];
         for (;;) {
             const bool from_list = nlist != kNone;
             if (from_list) {
@@ -607,10 +614,8 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
             if (cont == kNone) break;
             if (from_list) {
                 ++lpass;
-                if constexpr (!FRAME) {
-                    const uint32_t k0 = lpass * kListPerBlock;
-                    ent = k0 + lane < nlist ? *reinterpret_cast<const uint64_t*>(out + first_b + k0 + lane) : 0ull;
-                }
+                const uint32_t k0 = lpass * kListPerBlock;
+                ent = k0 + lane < nlist ? xlist[uint64_t(first_b + k0 + lane) * xstride] : 0ull;
             } else {
                 walk_from = cont;
             }
@@ -634,7 +639,9 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                                                                      revel_record_result* __restrict__ out,
                                                                      uint32_t lead,
                                                                      const uint64_t* __restrict__ hlist,
-                                                                     const uint32_t* __restrict__ counts) {
+                                                                     const uint32_t* __restrict__ counts,
+                                                                     const uint64_t* __restrict__ xlist,
+                                                                     uint32_t xstride) {
     __shared__ uint32_t tab[32768];
     __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
     fill_tables<TM_S4R>(tab);
@@ -647,7 +654,11 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     const uint64_t waves_per_wg = kVerify2Threads / 64;
     const uint64_t nwaves = gridDim.x * waves_per_wg;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
-    const bool use_list = hlist != nullptr && counts != nullptr;
+    // header lists: verify = the count pass's (records 0..63 in hlist, the
+    // rest listed by k_list_overflow into the result slots: xlist = out,
+    // stride 3 u64); FRAME = entry k of block b at xlist[first[b] + k]
+    // (written by k_scatter_fragments)
+    const bool use_list = counts != nullptr && (FRAME ? xlist != nullptr : hlist != nullptr);
     const uint32_t cs = lane * 512u, ce = cs + 512u;
 
     // wave-uniform block index (readfirstlane: the compiler cannot prove that
@@ -667,7 +678,12 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     auto prefetch = [&](uint64_t nb) {
         if (use_list) {
             pf_count = counts[nb];
-            pf_hl = hlist[nb * kListStride + lane];
+            if constexpr (FRAME) {
+                pf_first = first[nb];
+                pf_hl = lane < pf_count ? xlist[uint64_t(pf_first) + lane] : 0ull;
+            } else {
+                pf_hl = hlist[nb * kListStride + lane];
+            }
         }
         if constexpr (!FRAME) pf_first = first[nb];
         load_round(image + nb * kBlockSize - lead, cur, 0, true, 0u);
@@ -695,10 +711,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                 const uint32_t k0 = lpass * kRecCap2;
                 const uint32_t np = min(nlist - k0, kRecCap2);
                 uint64_t ent_b = 0;
-                if constexpr (!FRAME) {
-                    if (np > 64u && k0 + 64u + lane < nlist)
-                        ent_b = *reinterpret_cast<const uint64_t*>(out + first_b + k0 + 64u + lane);
-                }
+                if (np > 64u && k0 + 64u + lane < nlist)
+                    ent_b = xlist[uint64_t(first_b + k0 + 64u + lane) * xstride];
                 const Hdr h = list_header(ent), hb = list_header(ent_b);
                 const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
                 const uint32_t szb = lane + 64u < np ? kHeaderSize + hb.len : 0u;
@@ -865,10 +879,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             if (cont == kNone) break;
             if (from_list) {
                 ++lpass;
-                if constexpr (!FRAME) {
-                    const uint32_t k0 = lpass * kRecCap2;
-                    ent = k0 + lane < nlist ? *reinterpret_cast<const uint64_t*>(out + first_b + k0 + lane) : 0ull;
-                }
+                const uint32_t k0 = lpass * kRecCap2;
+                ent = k0 + lane < nlist ? xlist[uint64_t(first_b + k0 + lane) * xstride] : 0ull;
             } else {
                 walk_from = cont;
             }
@@ -883,7 +895,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 // wave per fragment; the layout comes from the host (frame_layout()).
 // ---------------------------------------------------------------------------
 __global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const revel::FragDesc* __restrict__ frags,
-                                    uint64_t nfrags, uint8_t* __restrict__ image) {
+                                    uint64_t nfrags, uint8_t* __restrict__ image, uint64_t* __restrict__ xlist) {
     // 8 fragments per wave visit: one of at most kSmallFragment payload bytes
     // (or a trailer) is written by its own 8-lane group, larger ones then by
     // the whole wave (group_copy: aligned 16-B stores)
@@ -906,6 +918,8 @@ __global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const 
             } else if (gl < kHeaderSize) {
                 const uint32_t hv = gl < 4 ? 0u : gl == 4 ? (d.len & 0xffu) : gl == 5 ? (d.len >> 8) : d.type;
                 dst[gl] = (uint8_t)hv;
+                // header-list entry of this record for the CRC pass (CRC still 0)
+                if (gl == 0 && xlist) xlist[f] = list_entry(Hdr{0u, d.len, d.type});
             }
         }
         const bool payload = f < nfrags && d.type != revel::kTrailer;
@@ -1014,15 +1028,20 @@ static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
 template <bool FRAME>
 static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
+                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st,
+                                 const uint64_t* xlist = nullptr, uint32_t xstride = 1) {
+    if (!FRAME) {  // entries past the first 64 of a block: in the result slots
+        xlist = reinterpret_cast<const uint64_t*>(d_out);
+        xstride = sizeof(revel_record_result) / 8;
+    }
     hipLaunchKernelGGL((k_verify_records3<FRAME>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st, img, nbytes,
-                       base_offset, d_first, d_out, lead, hl, d_counts);
+                       base_offset, d_first, d_out, lead, hl, d_counts, xlist, xstride);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !partial) return e;
     // <= 2 partial blocks: one single-wave workgroup each, 4 KiB unreplicated tables
     // (a 128 KiB table fill and one latency-bound wave cost ~50 us per launch)
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64>), dim3(2), dim3(64), 0, st, img,
-                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
+                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xlist, xstride);
     return hipGetLastError();
 }
 
@@ -1031,11 +1050,12 @@ static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                  uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_WHOLE>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts);
+                       img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts,
+                       reinterpret_cast<const uint64_t*>(d_out), 3u);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !partial) return e;
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img, nbytes,
-                       base_offset, d_first, d_out, lead, hl, d_counts);
+                       base_offset, d_first, d_out, lead, hl, d_counts, reinterpret_cast<const uint64_t*>(d_out), 3u);
     return hipGetLastError();
 }
 
@@ -1073,7 +1093,8 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
                                                              0u, hl, d_counts, st);
         case 5:  // round-1 production: one kernel for whole and partial blocks
             hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
-                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts);
+                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                               reinterpret_cast<const uint64_t*>(d_out), 3u);
             return hipGetLastError();
         case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
                                                        hl, d_counts, st);
@@ -1106,11 +1127,13 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
 }
 
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
-                         void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st) {
+                         void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st, const uint32_t* d_counts,
+                         const uint32_t* d_first, uint64_t* d_xlist) {
     if (nfrags) {
         const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (nfrags + 31) / 32));
         hipLaunchKernelGGL(k_scatter_fragments, dim3((uint32_t)grid), dim3(256), 0, st,
-                           static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image));
+                           static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image),
+                           d_xlist);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1121,8 +1144,10 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     const bool partial = lead != 0 || (image_len + lead) % kBlockSize != 0;
-    return launch_verify3<true>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull, nullptr, nullptr,
-                                lead, nullptr, nullptr, st);
+    const bool lists = d_counts && d_first && d_xlist;
+    return launch_verify3<true>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull,
+                                lists ? d_first : nullptr, nullptr, lead, nullptr, lists ? d_counts : nullptr, st,
+                                lists ? d_xlist : nullptr, 1u);
 }
 
 }  // namespace revel
