@@ -509,9 +509,12 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const uint32_t p16 = cs + rr * 128 + j * 16;
-                        // don't-care gap before the next record, or strictly inside one
+                        // don't-care bytes before the next record, or inside one
                         const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
                         if (BP != BP_MASK_NOVOTE && __all(interior)) {
+                            // a record starting exactly here: the register may hold garbage
+                            // from don't-care bytes (bytes of records outside this list batch)
+                            state = p16 == s ? 0u : state;
                             state = absorb4<TM>(state, cur[j], L, tab);
                         } else if constexpr (BP != BP_BYTES) {
                             const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
@@ -792,9 +795,12 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const uint32_t p16 = cs + rr * 128 + j * 16;
-                        // don't-care gap before the next record, or strictly inside one
+                        // don't-care bytes before the next record, or inside one
                         const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
                         if (__all(interior)) {
+                            // a record starting exactly here: the register may hold garbage
+                            // from don't-care bytes (bytes of records outside this list batch)
+                            state = p16 == s ? 0u : state;
                             state = absorb4<TM_S4R>(state, cur[j], L, tab);
                         } else {
                             const uint32_t ws[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};

@@ -223,6 +223,25 @@ def test_verify_multi_batch_lists(gpu_ctx, rec_len):
     assert (ref2["status"] == 1).sum() > 10
 
 
+def test_verify_batch_start_on_16_byte_boundary(gpu_ctx):
+    """16-B records after a first record of every size 0..15: the first record
+    of some list batch then starts exactly on a 16-B segment of a lane that has
+    absorbed bytes of the previous batch's records (the fast path must not
+    carry that register into the record; found by the dense append test)."""
+    for period, l0 in [(p, l) for p in (32, 64) for l in range(16)]:
+        # record k >= 1 starts at 7 + l0 + (k - 1) * period: with l0 = 3 the first
+        # record of every 64- / 128-record batch starts 16 bytes before a
+        # 512-B lane chunk ends (s = 4096 t - 16 for period 32)
+        rng = np.random.default_rng(l0)
+        recs = [rng.integers(0, 256, l0, dtype=np.uint8).tobytes()]
+        recs += [rng.integers(0, 256, period - 7, dtype=np.uint8).tobytes() for _ in range(3000)]
+        img = oc.write_image(recs)
+        dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+        ref = oc.walk(img)
+        for v in VERIFY_VARIANTS:
+            compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref)
+
+
 def test_verify_base_offset_and_random_bytes(gpu_ctx):
     rng = np.random.default_rng(14)
     img = rng.integers(0, 256, 5 * BLOCK_SIZE + 123, dtype=np.uint8).tobytes()  # garbage headers
@@ -395,6 +414,21 @@ def test_append_records_matches_writer(gpu_ctx, block_offset):
     for r in recs:
         w.add_record(r)
     assert bo == w.block_offset
+    assert n == len(want)
+    assert gpu_ctx.d2h(img, n).tobytes() == want
+
+
+@pytest.mark.parametrize("block_offset", [0, 5, 32000])
+def test_append_records_dense_blocks(gpu_ctx, block_offset):
+    """~900 records per block: the framing header lists run in several
+    128-record batches per whole block and 64-record batches in the lead and
+    tail blocks."""
+    rng = np.random.default_rng(block_offset + 77)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 60, 4000)]
+    blob = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    d = gpu_ctx.upload(blob)
+    img, n, bo = gpu_ctx.append_records(d, [len(r) for r in recs], block_offset)
+    want = oc.write_image(recs, block_offset)
     assert n == len(want)
     assert gpu_ctx.d2h(img, n).tobytes() == want
 
