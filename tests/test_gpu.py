@@ -648,6 +648,39 @@ def test_property_random_streams_vs_oracle(gpu_ctx):
     prop()
 
 
+def test_property_dense_streams_vs_oracle(gpu_ctx):
+    """Hypothesis: dense streams (hundreds to thousands of small records, so
+    blocks hold several header-list batches), a periodic tail that puts batch
+    starts on fixed alignments, optional bit flips -> every verify variant and
+    the device append framing (at a random block offset) equal the oracle."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as hs
+
+    @settings(max_examples=30, deadline=None, suppress_health_check=list(HealthCheck), derandomize=True)
+    @given(n=hs.integers(100, 3000), maxlen=hs.integers(1, 120), period=hs.integers(0, 60),
+           seed=hs.integers(0, 2**32 - 1), flips=hs.integers(0, 5), block_offset=hs.integers(0, 32768))
+    def prop(n, maxlen, period, seed, flips, block_offset):
+        rng = np.random.default_rng(seed)
+        sizes = rng.integers(0, maxlen + 1, n)
+        if period:
+            sizes[n // 2:] = period
+        recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+        img = bytearray(oc.write_image(recs))
+        for _ in range(flips):
+            img[int(rng.integers(0, len(img)))] ^= 1 << int(rng.integers(0, 8))
+        img = bytes(img)
+        d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+        ref = oc.walk(img)
+        for v in VERIFY_VARIANTS:
+            compare_walk(gpu_ctx.verify_image(d, len(img), variant=v), ref)
+        blob = np.frombuffer(b"".join(recs) or b"\0", dtype=np.uint8)
+        dp = gpu_ctx.upload(blob)
+        fimg, fn, _ = gpu_ctx.append_records(dp, [len(r) for r in recs], block_offset)
+        assert gpu_ctx.d2h(fimg, fn).tobytes() == oc.write_image(recs, block_offset)
+
+    prop()
+
+
 def test_property_batch_decode_mutations(gpu_ctx):
     """Hypothesis: WriteBatch logs whose batch bytes are mutated before framing
     (valid log records carrying malformed batches) -> device decode == oracle."""
