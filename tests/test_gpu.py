@@ -677,6 +677,11 @@ def test_property_dense_streams_vs_oracle(gpu_ctx):
         dp = gpu_ctx.upload(blob)
         fimg, fn, _ = gpu_ctx.append_records(dp, [len(r) for r in recs], block_offset)
         assert gpu_ctx.d2h(fimg, fn).tobytes() == oc.write_image(recs, block_offset)
+        # the GPU reader (count -> scan -> verify per window) and the replay summary
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=True, gpu=gpu_ctx, window_bytes=65536)
+        assert drain(rd.read_record) == drain(po.LogReader(img, True, 0).read_record)
+        st = gpu_ctx.replay_memory(img, window_bytes=65536)
+        assert (st["units"], st["bad"]) == (len(ref), int((ref["status"] != 0).sum()))
 
     prop()
 
