@@ -627,6 +627,31 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
+// The blocks b0, b0 + step, ... < hi of one wave whose record count is above
+// kListPerBlock (DENSE) or at most kListPerBlock (!DENSE): one vector load of
+// 64 candidates' counts, then one set bit of the ballot per block.  Every
+// member is wave-uniform.
+// ---------------------------------------------------------------------------
+template <bool DENSE>
+struct BlockSeq {
+    uint64_t scan, base, mask, step, hi;
+    __device__ BlockSeq(uint64_t b0, uint64_t step_, uint64_t hi_) : scan(b0), base(0), mask(0), step(step_), hi(hi_) {}
+    __device__ uint64_t next(const uint32_t* __restrict__ counts) {
+        while (mask == 0) {
+            if (scan >= hi) return hi;
+            const uint64_t c = scan + uint64_t(lane_id()) * step;
+            const bool sel = c < hi && ((counts[c] > kListPerBlock) == DENSE);
+            mask = __ballot(sel);
+            base = scan;
+            scan += 64u * step;
+        }
+        const uint32_t i = (uint32_t)__builtin_ctzll(mask);
+        mask &= mask - 1u;
+        return base + uint64_t(i) * step;
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Config C3, v3 (production, whole blocks): v2's per-block work, software-
 // pipelined across the blocks a wave visits.  After a block's main loop the
 // wave issues the finalizer's header loads, then the NEXT block's round-0
@@ -635,7 +660,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 // finalized, so a block no longer pays three global round trips in series.
 // Partial blocks (first/last) still go through k_verify_records2<.., BS_PARTIAL>.
 // ---------------------------------------------------------------------------
-template <bool FRAME>
+template <bool FRAME, bool DENSE = false>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -667,7 +692,10 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     // wave-uniform block index (readfirstlane: the compiler cannot prove that
     // threadIdx.x >> 6 is uniform, and would keep the block arithmetic in VGPRs)
     const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint64_t b = b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
+    // DENSE: only the blocks with more than kListPerBlock records (the rest
+    // went through the coalesced k_verify_records5)
+    BlockSeq<true> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg, nwaves, b_hi);
+    uint64_t b = DENSE ? seq.next(counts) : b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
     if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
     uint4 cur[8], nxt[8];
     uint32_t pf_count = kNone, pf_first = 0;
@@ -695,7 +723,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     while (b < b_hi) {
         const uint64_t base = b * kBlockSize;
         const uint8_t* blk = image + base - lead;
-        const uint64_t bn = b + nwaves;
+        const uint64_t bn = DENSE ? seq.next(counts) : b + nwaves;
         const uint32_t nlist = pf_count;
         uint64_t ent = pf_hl;  // this lane's header-list entry of the current batch
         const uint32_t first_b = __builtin_amdgcn_readfirstlane(pf_first);
@@ -895,6 +923,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     }
 }
 
+#include "verify5.inc"
+
 // ---------------------------------------------------------------------------
 // Device append framing, step 1: scatter fragments (payload bytes + length
 // and type header bytes, CRC left zero) and zero the block trailers.  One
@@ -1051,6 +1081,34 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
     return hipGetLastError();
 }
 
+// v5: the coalesced kernel over the whole blocks with <= kListPerBlock records,
+// v3 over the denser ones (each skips the other's blocks by their counts),
+// then the partial first/last block as in launch_verify3.
+static hipError_t launch_verify5(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
+                                 const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
+                                 const uint32_t* d_counts, hipStream_t st) {
+    const uint64_t whole = nbytes / kBlockSize;
+    if (whole) {
+        const uint64_t w5 = kV5Threads / 64, w3 = kVerify2Threads / 64;
+        const uint64_t g5 = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (whole + w5 - 1) / w5));
+        hipLaunchKernelGGL(k_verify_records5, dim3((uint32_t)g5), dim3(kV5Threads), 0, st, img, nbytes, base_offset,
+                           d_first, d_out, hl, d_counts);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const uint64_t g3 = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (whole + w3 - 1) / w3));
+        hipLaunchKernelGGL((k_verify_records3<false, true>), dim3((uint32_t)g3), dim3(kVerify2Threads), 0, st, img,
+                           nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                           reinterpret_cast<const uint64_t*>(d_out), (uint32_t)(sizeof(revel_record_result) / 8));
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (nbytes % kBlockSize == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_PARTIAL, TM_S4, 64>), dim3(2), dim3(64), 0, st, img,
+                       nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, reinterpret_cast<const uint64_t*>(d_out),
+                       (uint32_t)(sizeof(revel_record_result) / 8));
+    return hipGetLastError();
+}
+
 template <bool FRAME, int BP>
 static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
@@ -1104,6 +1162,8 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return hipGetLastError();
         case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
                                                        hl, d_counts, st);
+        case 7: return hl && d_counts ? launch_verify5(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, st)
+                                      : hipErrorInvalidValue;
         case 0:
         case 2: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
                                              d_counts, st);

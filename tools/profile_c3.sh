@@ -7,7 +7,7 @@ O=$R/gpurun_out/c3prof_$tag
 mkdir -p "$O"
 export TMPDIR=/tmp
 step() { "$R/tools/box_step.sh" "$@" || exit 99; }
-W="python3 $R/tools/bench_c3.py --variants 0 --iters 2"
+W="python3 $R/tools/bench_c3.py --variants ${C3_VARIANT:-0} --iters 2 ${C3_ARGS:-}"
 i=0
 for grp in "FETCH_SIZE" \
            "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
