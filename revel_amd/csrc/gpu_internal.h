@@ -31,12 +31,16 @@ hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void
 hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st);
 hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
                              hipStream_t st);
-// d_hlist (nullable): nblocks * kListStride u64 per block for verify: the 7
-// header bytes of each of the block's first kListPerBlock records, then the
-// in-block offset of record kListPerBlock when there are more (verify lists
-// the rest into its result slots, k_list_overflow).
+// d_hlist (nullable): kListStride u64 per block for verify: the 7 header
+// bytes of each of the block's first kListCap records, then the in-block
+// offset of record kListCap when there are more (verify lists the rest into
+// its result slots, k_list_overflow).  kListCap covers db_bench-shaped logs
+// (~240 records of ~140 B per block) in the count pass's one walk.
+// kListPerBlock = records per list batch (one per lane) and the density
+// threshold: blocks with more go to k_verify_records_dense.
 constexpr uint32_t kListPerBlock = 64;
-constexpr uint32_t kListStride = kListPerBlock + 1;
+constexpr uint32_t kListCap = 256;
+constexpr uint32_t kListStride = kListCap + 1;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st);
 // d_tile_scratch: scan_scratch_words(n) u32 of device scratch.

@@ -14,9 +14,9 @@ using namespace revel;
 
 namespace {
 // Per block (one lane each): number of physical records and, when list is
-// non-null, the first kListPerBlock headers (list_entry; the walk stops at the
+// non-null, the first kListCap headers (list_entry; the walk stops at the
 // first bad header, so only the last entry can be bad) followed by the in-block
-// offset of record kListPerBlock when the block has more records.
+// offset of record kListCap when the block has more records.
 __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts,
                                 uint64_t* __restrict__ hlist) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
@@ -29,8 +29,8 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
         while (bl - off >= kHeaderSize) {
             const Hdr h = read_header(blk, off, bl);
             const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-            if (hlist && n < kListPerBlock) hlist[b * kListStride + n] = list_entry(h);
-            if (hlist && n == kListPerBlock) hlist[b * kListStride + kListPerBlock] = off;  // resume point
+            if (hlist && n < kListCap) hlist[b * kListStride + n] = list_entry(h);
+            if (hlist && n == kListCap) hlist[b * kListStride + kListCap] = off;  // resume point
             ++n;
             if (!ok) break;
             off += kHeaderSize + h.len;
@@ -39,7 +39,7 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 
-// Header-list entries of records kListPerBlock.. of the blocks that have more
+// Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
 // resuming at the offset the count pass left.  Entry k of block b goes into the
 // first 8 bytes of its own 24-byte result slot out[first[b] + k]: the verify
@@ -51,13 +51,13 @@ __global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbyt
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
          b += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t n = counts[b];
-        if (n <= kListPerBlock) continue;
+        if (n <= kListCap) continue;
         const uint64_t base = b * kBlockSize;
         const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
         const uint8_t* blk = image + base;
-        uint32_t off = (uint32_t)hlist[b * kListStride + kListPerBlock];
+        uint32_t off = (uint32_t)hlist[b * kListStride + kListCap];
         uint64_t* slot = reinterpret_cast<uint64_t*>(out + first[b]);
-        for (uint32_t k = kListPerBlock; k < n; ++k) {
+        for (uint32_t k = kListCap; k < n; ++k) {
             const Hdr h = read_header(blk, off, bl);
             slot[k * (sizeof(revel_record_result) / 8)] = list_entry(h);
             off += kHeaderSize + h.len;  // only the last record can be bad
@@ -307,6 +307,16 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify_records(const uint8_t
 constexpr int kVerify2Threads = 1024;
 constexpr uint32_t kRecCap2 = 128;  // >= kListPerBlock
 
+// Header-list entry k of block b.  Verify: the count pass kept k < kListCap in
+// hlist, k_list_overflow wrote the rest into the result slots (xlist = out,
+// xstride u64 apart).  FRAME: the framing list holds every entry in xlist.
+template <bool FRAME>
+__device__ __forceinline__ uint64_t list_at(const uint64_t* __restrict__ hlist, const uint64_t* __restrict__ xlist,
+                                            uint32_t xstride, uint64_t b, uint32_t first_b, uint32_t k) {
+    if (!FRAME && k < kListCap) return hlist[b * kListStride + k];
+    return xlist[uint64_t(first_b + k) * xstride];
+}
+
 // x^(8d) and init_xor(d) for d = 0..32768, filled once per device.
 __device__ uint32_t g_x8n_tab[kBlockSize + 1];
 __device__ uint32_t g_init_xor_tab[kBlockSize + 1];
@@ -380,7 +390,8 @@ enum BoundaryPath : int { BP_BYTES = 0, BP_MASK = 1, BP_MASK_NOVOTE = 2 };
 // mid-block, and the last), launched as one extra workgroup.
 enum BlockSet : int { BS_ALL = 0, BS_WHOLE = 1, BS_PARTIAL = 2 };
 
-template <bool FRAME, int BP = BP_BYTES, int WHICH = BS_ALL, int TM = TM_S4R, int THREADS = kVerify2Threads>
+template <bool FRAME, int BP = BP_BYTES, int WHICH = BS_ALL, int TM = TM_S4R, int THREADS = kVerify2Threads,
+          bool SPARSE_ONLY = false>
 __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -416,6 +427,9 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
             if (bl != kBlockSize || lo_b != 0) continue;
         } else if constexpr (WHICH == BS_PARTIAL) {
             if (bl == kBlockSize && lo_b == 0) continue;
+        }
+        if constexpr (SPARSE_ONLY) {  // a dense partial block went to k_verify_records_dense
+            if (counts[b] > kListPerBlock) continue;
         }
         const uint32_t cs = lane * 512u, ce = cs + 512u;
         uint32_t out_base = FRAME ? 0u : first[b];
@@ -618,7 +632,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
             if (from_list) {
                 ++lpass;
                 const uint32_t k0 = lpass * kListPerBlock;
-                ent = k0 + lane < nlist ? xlist[uint64_t(first_b + k0 + lane) * xstride] : 0ull;
+                ent = k0 + lane < nlist ? list_at<FRAME>(hlist, xlist, xstride, b, first_b, k0 + lane) : 0ull;
             } else {
                 walk_from = cont;
             }
@@ -634,20 +648,20 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 // ---------------------------------------------------------------------------
 template <bool DENSE>
 struct BlockSeq {
-    uint64_t scan, base, mask, step, hi;
-    __device__ BlockSeq(uint64_t b0, uint64_t step_, uint64_t hi_) : scan(b0), base(0), mask(0), step(step_), hi(hi_) {}
-    __device__ uint64_t next(const uint32_t* __restrict__ counts) {
+    uint32_t scan;  // first candidate not yet in mask (block indices fit 32 bits: 128 TiB images)
+    uint64_t mask;  // qualifying blocks among scan - 64 step .. scan - step
+    __device__ explicit BlockSeq(uint64_t b0) : scan((uint32_t)b0), mask(0) {}
+    __device__ uint64_t next(const uint32_t* __restrict__ counts, uint64_t step, uint64_t hi) {
         while (mask == 0) {
             if (scan >= hi) return hi;
             const uint64_t c = scan + uint64_t(lane_id()) * step;
             const bool sel = c < hi && ((counts[c] > kListPerBlock) == DENSE);
             mask = __ballot(sel);
-            base = scan;
-            scan += 64u * step;
+            scan += (uint32_t)(64u * step);
         }
         const uint32_t i = (uint32_t)__builtin_ctzll(mask);
         mask &= mask - 1u;
-        return base + uint64_t(i) * step;
+        return scan - 64u * step + uint64_t(i) * step;
     }
 };
 
@@ -660,7 +674,9 @@ struct BlockSeq {
 // finalized, so a block no longer pays three global round trips in series.
 // Partial blocks (first/last) still go through k_verify_records2<.., BS_PARTIAL>.
 // ---------------------------------------------------------------------------
-template <bool FRAME, bool DENSE = false>
+enum BlockSel : int { SEL_ALL = 0, SEL_DENSE = 1, SEL_SPARSE = 2 };
+
+template <bool FRAME, int SEL = SEL_ALL>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -692,10 +708,10 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     // wave-uniform block index (readfirstlane: the compiler cannot prove that
     // threadIdx.x >> 6 is uniform, and would keep the block arithmetic in VGPRs)
     const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // DENSE: only the blocks with more than kListPerBlock records (the rest
-    // went through the coalesced k_verify_records5)
-    BlockSeq<true> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg, nwaves, b_hi);
-    uint64_t b = DENSE ? seq.next(counts) : b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
+    // SEL_SPARSE / SEL_DENSE: only the blocks with at most / more than
+    // kListPerBlock records (the others go to k_verify_records_dense / v5)
+    BlockSeq<SEL == SEL_DENSE> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg);
+    uint64_t b = SEL != SEL_ALL ? seq.next(counts, nwaves, b_hi) : b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
     if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
     uint4 cur[8], nxt[8];
     uint32_t pf_count = kNone, pf_first = 0;
@@ -723,7 +739,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     while (b < b_hi) {
         const uint64_t base = b * kBlockSize;
         const uint8_t* blk = image + base - lead;
-        const uint64_t bn = DENSE ? seq.next(counts) : b + nwaves;
+        const uint64_t bn = SEL != SEL_ALL ? seq.next(counts, nwaves, b_hi) : b + nwaves;
         const uint32_t nlist = pf_count;
         uint64_t ent = pf_hl;  // this lane's header-list entry of the current batch
         const uint32_t first_b = __builtin_amdgcn_readfirstlane(pf_first);
@@ -743,7 +759,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                 const uint32_t np = min(nlist - k0, kRecCap2);
                 uint64_t ent_b = 0;
                 if (np > 64u && k0 + 64u + lane < nlist)
-                    ent_b = xlist[uint64_t(first_b + k0 + 64u + lane) * xstride];
+                    ent_b = list_at<FRAME>(hlist, xlist, xstride, b, first_b, k0 + 64u + lane);
                 const Hdr h = list_header(ent), hb = list_header(ent_b);
                 const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
                 const uint32_t szb = lane + 64u < np ? kHeaderSize + hb.len : 0u;
@@ -914,7 +930,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
             if (from_list) {
                 ++lpass;
                 const uint32_t k0 = lpass * kRecCap2;
-                ent = k0 + lane < nlist ? xlist[uint64_t(first_b + k0 + lane) * xstride] : 0ull;
+                ent = k0 + lane < nlist ? list_at<FRAME>(hlist, xlist, xstride, b, first_b, k0 + lane) : 0ull;
             } else {
                 walk_from = cont;
             }
@@ -924,6 +940,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 }
 
 #include "verify5.inc"
+#include "verify_dense.inc"
 
 // ---------------------------------------------------------------------------
 // Device append framing, step 1: scatter fragments (payload bytes + length
@@ -1081,31 +1098,39 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
     return hipGetLastError();
 }
 
-// v5: the coalesced kernel over the whole blocks with <= kListPerBlock records,
-// v3 over the denser ones (each skips the other's blocks by their counts),
-// then the partial first/last block as in launch_verify3.
-static hipError_t launch_verify5(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
-                                 const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
-                                 const uint32_t* d_counts, hipStream_t st) {
-    const uint64_t whole = nbytes / kBlockSize;
+// Verify split by block density (counts from the count pass): the whole
+// blocks with <= kListPerBlock records through v3 (SPARSE_V5: the v5
+// experiment), every block with more (the partial last one too) through
+// k_verify_records_dense, and a sparse partial last block through the
+// single-wave verify2 launch.  Each kernel skips the others' blocks by count.
+template <bool SPARSE_V5>
+static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
+                                      const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
+                                      const uint32_t* d_counts, hipStream_t st) {
+    const uint64_t whole = nbytes / kBlockSize, nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t* xl = reinterpret_cast<const uint64_t*>(d_out);
+    const uint32_t xs = (uint32_t)(sizeof(revel_record_result) / 8);
+    auto grid_for = [&](uint64_t n, uint64_t waves) {
+        return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + waves - 1) / waves));
+    };
     if (whole) {
-        const uint64_t w5 = kV5Threads / 64, w3 = kVerify2Threads / 64;
-        const uint64_t g5 = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (whole + w5 - 1) / w5));
-        hipLaunchKernelGGL(k_verify_records5, dim3((uint32_t)g5), dim3(kV5Threads), 0, st, img, nbytes, base_offset,
-                           d_first, d_out, hl, d_counts);
+        if constexpr (SPARSE_V5) {
+            hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(whole, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
+                               nbytes, base_offset, d_first, d_out, hl, d_counts);
+        } else {
+            hipLaunchKernelGGL((k_verify_records3<false, SEL_SPARSE>), dim3(grid_for(whole, kVerify2Threads / 64)),
+                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                               xl, xs);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        const uint64_t g3 = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (whole + w3 - 1) / w3));
-        hipLaunchKernelGGL((k_verify_records3<false, true>), dim3((uint32_t)g3), dim3(kVerify2Threads), 0, st, img,
-                           nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                           reinterpret_cast<const uint64_t*>(d_out), (uint32_t)(sizeof(revel_record_result) / 8));
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
     }
-    if (nbytes % kBlockSize == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_PARTIAL, TM_S4, 64>), dim3(2), dim3(64), 0, st, img,
-                       nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, reinterpret_cast<const uint64_t*>(d_out),
-                       (uint32_t)(sizeof(revel_record_result) / 8));
+    hipLaunchKernelGGL(k_verify_records_dense, dim3(grid_for(nblocks, kDenseThreads / 64)), dim3(kDenseThreads), 0, st,
+                       img, nbytes, base_offset, d_first, d_out, hl, d_counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nbytes % kBlockSize == 0) return e;
+    hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st,
+                       img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl, xs);
     return hipGetLastError();
 }
 
@@ -1142,7 +1167,7 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
     const uint64_t* hl = variant == 2 ? nullptr : d_hlist;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
     if (hl && d_counts) {
-        // list the headers of blocks with more than kListPerBlock records
+        // list the headers of blocks with more than kListCap records
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
         hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
                            d_out);
@@ -1162,9 +1187,14 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return hipGetLastError();
         case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
                                                        hl, d_counts, st);
-        case 7: return hl && d_counts ? launch_verify5(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, st)
+        case 7: return hl && d_counts ? launch_verify_split<true>(di, img, nbytes, base_offset, d_first, d_out, hl,
+                                                                  d_counts, st)
                                       : hipErrorInvalidValue;
         case 0:
+            if (hl && d_counts)
+                return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, st);
+            [[fallthrough]];
+        case 8:  // session-2 production: v3 over every whole block
         case 2: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
                                              d_counts, st);
         default: return hipErrorInvalidValue;
