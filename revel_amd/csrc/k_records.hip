@@ -1098,41 +1098,47 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
     return hipGetLastError();
 }
 
-// Verify split by block density (counts from the count pass): the whole
-// blocks with <= kListPerBlock records through v3 (SPARSE_V5: the v5
-// experiment), every block with more (the partial last one too) through
-// k_verify_records_dense, and a sparse partial last block through the
-// single-wave verify2 launch.  Each kernel skips the others' blocks by count.
-template <bool SPARSE_V5>
+// Verify (or FRAME: append framing) split by block density, from the
+// per-block record counts: the whole blocks with <= kListPerBlock records
+// through v3 (SPARSE_V5: the v5 experiment; verify only), every block with
+// more (partial first / last ones too) through k_verify_records_dense, and the
+// sparse partial blocks through the single-wave verify2 launch.  Each kernel
+// skips the others' blocks by count.  Lists: verify = hlist + overflow entries
+// in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
+template <bool FRAME, bool SPARSE_V5 = false>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
-                                      const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
-                                      const uint32_t* d_counts, hipStream_t st) {
-    const uint64_t whole = nbytes / kBlockSize, nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    const uint64_t* xl = reinterpret_cast<const uint64_t*>(d_out);
-    const uint32_t xs = (uint32_t)(sizeof(revel_record_result) / 8);
+                                      const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
+                                      const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
+                                      hipStream_t st) {
+    const uint64_t vbytes = nbytes + lead;
+    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize, nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
     auto grid_for = [&](uint64_t n, uint64_t waves) {
         return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + waves - 1) / waves));
     };
-    if (whole) {
+    if (b_hi > b_lo) {
         if constexpr (SPARSE_V5) {
-            hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(whole, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
+            static_assert(!FRAME, "v5 verifies only");
+            hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(b_hi, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
                                nbytes, base_offset, d_first, d_out, hl, d_counts);
         } else {
-            hipLaunchKernelGGL((k_verify_records3<false, SEL_SPARSE>), dim3(grid_for(whole, kVerify2Threads / 64)),
-                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                               xl, xs);
+            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
+                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
+                               d_counts, xl, xs);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_verify_records_dense, dim3(grid_for(nblocks, kDenseThreads / 64)), dim3(kDenseThreads), 0, st,
-                       img, nbytes, base_offset, d_first, d_out, hl, d_counts);
+    hipLaunchKernelGGL(k_verify_records_dense<FRAME>, dim3(grid_for(nblocks, kDenseThreads / 64)), dim3(kDenseThreads),
+                       0, st, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || nbytes % kBlockSize == 0) return e;
-    hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st,
-                       img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl, xs);
+    if (e != hipSuccess || (lead == 0 && vbytes % kBlockSize == 0)) return e;
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st, img,
+                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs);
     return hipGetLastError();
 }
+
+// the dense kernel reads aligned 16 B relative to the image start
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 template <bool FRAME, int BP>
 static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
@@ -1187,12 +1193,16 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return hipGetLastError();
         case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
                                                        hl, d_counts, st);
-        case 7: return hl && d_counts ? launch_verify_split<true>(di, img, nbytes, base_offset, d_first, d_out, hl,
-                                                                  d_counts, st)
-                                      : hipErrorInvalidValue;
+        case 7:
+            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
+            return launch_verify_split<false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                                                    reinterpret_cast<const uint64_t*>(d_out),
+                                                    (uint32_t)(sizeof(revel_record_result) / 8), st);
         case 0:
-            if (hl && d_counts)
-                return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, st);
+            if (hl && d_counts && aligned16(img))
+                return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                                                  reinterpret_cast<const uint64_t*>(d_out),
+                                                  (uint32_t)(sizeof(revel_record_result) / 8), st);
             [[fallthrough]];
         case 8:  // session-2 production: v3 over every whole block
         case 2: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
@@ -1241,6 +1251,9 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     const bool partial = lead != 0 || (image_len + lead) % kBlockSize != 0;
     const bool lists = d_counts && d_first && d_xlist;
+    if (lists && aligned16(d_image))
+        return launch_verify_split<true>(di, static_cast<const uint8_t*>(d_image), image_len, 0ull, d_first, nullptr,
+                                         lead, nullptr, d_counts, d_xlist, 1u, st);
     return launch_verify3<true>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull,
                                 lists ? d_first : nullptr, nullptr, lead, nullptr, lists ? d_counts : nullptr, st,
                                 lists ? d_xlist : nullptr, 1u);
