@@ -242,6 +242,71 @@ def test_verify_batch_start_on_16_byte_boundary(gpu_ctx):
             compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref)
 
 
+class _View:
+    """A device image at a byte offset inside a larger buffer."""
+
+    def __init__(self, buf, off, nbytes):
+        self.ptr, self.nbytes, self._buf = buf.ptr + off, nbytes, buf
+
+
+def _density_mix(seed, tail):
+    """Blocks alternating dense (24..140-B records, > 64 per block) and sparse
+    (2..30 KiB records) runs; `tail` picks the record sizes that end the image
+    (a dense or a sparse partial last block)."""
+    rng = np.random.default_rng(seed)
+    recs = []
+    for run in range(6):
+        dense = run % 2 == 0
+        total = 0
+        while total < (BLOCK_SIZE if dense else 2 * BLOCK_SIZE):
+            n = int(rng.integers(24, 140)) if dense else int(rng.integers(2000, 30000))
+            recs.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+            total += n + 7
+    for _ in range(200 if tail == "dense" else 1):
+        n = int(rng.integers(10, 100)) if tail == "dense" else 9000
+        recs.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    return oc.write_image(recs)
+
+
+@pytest.mark.parametrize("tail", ["dense", "sparse"])
+def test_verify_mixed_density(gpu_ctx, tail):
+    """The production split (v3 over blocks with <= 64 records, the per-record
+    dense kernel over the rest, partial last block by its density) on one
+    image holding both kinds, with bit flips in both, vs the oracle."""
+    img = bytearray(_density_mix(7 if tail == "dense" else 8, tail))
+    ref = oc.walk(bytes(img))
+    counts = np.bincount((ref["file_offset"] // BLOCK_SIZE).astype(np.int64))
+    assert (counts > 64).any() and (counts <= 64).any()
+    rng = np.random.default_rng(3)
+    for v in rng.choice(len(ref) - 1, 40, replace=False):
+        off = int(ref["file_offset"][v]) + 7 + int(rng.integers(0, max(1, int(ref["length"][v]))))
+        if off < len(img):
+            img[off] ^= 0x10
+    img = bytes(img)
+    ref = oc.walk(img)
+    assert (ref["status"] == 1).sum() > 10
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    for v in (0, 7, 8):
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref)
+
+
+@pytest.mark.parametrize("shift", [1, 4, 8, 12, 16])
+def test_verify_unaligned_image_base(gpu_ctx, shift):
+    """An image that does not start on a 16-B boundary: the split path reads
+    aligned 16 B relative to the image, so such images take the previous
+    kernels (variant 0 falls back, variant 7 refuses); results unchanged."""
+    img = _density_mix(11, "dense")
+    buf = gpu_ctx.alloc(len(img) + 64)
+    gpu_ctx.h2d(buf, np.frombuffer(img, dtype=np.uint8), dst_offset=shift)
+    view = _View(buf, shift, len(img))
+    ref = oc.walk(img)
+    for v in (0, 8):
+        compare_walk(gpu_ctx.verify_image(view, len(img), variant=v), ref)
+    if shift % 16:
+        with pytest.raises(RevelError):
+            gpu_ctx.verify_image(view, len(img), variant=7)
+
+
 def test_verify_base_offset_and_random_bytes(gpu_ctx):
     rng = np.random.default_rng(14)
     img = rng.integers(0, 256, 5 * BLOCK_SIZE + 123, dtype=np.uint8).tobytes()  # garbage headers
