@@ -132,6 +132,7 @@ def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
         got = oracle_c.full_block_crcs(sample, v)
         ctxt[v] = round(len(idx) * BLOCK_SIZE / 2**30 / (time.perf_counter() - t0), 3)
         parity = parity and bool(np.array_equal(got, gpu_crc))
+    allcore = cpu_allcore(oracle_c, sample)
     c1 = c1_reference_path(oracle_c)
     return {
         "value": round(done * BLOCK_SIZE / 2**30 / t_byte, 4),
@@ -142,10 +143,54 @@ def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
                   f" cycled for {t_byte:.1f} s = {done} block CRCs; oracle bytewise 256-entry table CRC "
                   f"(crate `crc` algorithm class), single thread",
         "context_GiB_s_1core": ctxt,
+        "context_GiB_s_allcore": allcore,
         "host_cores_available": os.cpu_count(),
         "parity_vs_gpu": parity,
         "c1_reference_path": c1,
     }
+
+
+def cpu_allcore(oracle_c, sample, seconds: float = 1.5):
+    """SURVEY 8(d)'s all-core line: one independent block stream per host
+    thread (the reference's Writer/Reader are single-threaded per stream), each
+    thread cycling over its own slice of the sample for ~`seconds`, per CRC
+    implementation.  Threads = the host CPUs this process may use, capped at
+    16 (a one-GPU box's CPU share).  Context only: `value` stays one core."""
+    import threading
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    nt = max(1, min(16, avail))
+    out = {"threads": nt}
+    for v in ("bytewise", "slice16", "sse42"):
+        done = [0] * nt
+        t_end = [0.0]
+
+        per = max(1, len(sample) // nt)
+
+        def work(t):
+            lo = min(t * per, len(sample) - per)
+            part = sample[lo:lo + per]  # contiguous: no copy inside the timed calls
+            k, j, n = 0, 0, 0
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < seconds:
+                m = min(64, len(part) - j)
+                oracle_c.full_block_crcs(part[j:j + m], v)  # ctypes releases the GIL
+                n += m
+                j = (j + m) % len(part)
+                k += 1
+            done[t] = n
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(nt)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        t_end[0] = time.perf_counter() - t0
+        out[v] = round(sum(done) * BLOCK_SIZE / 2**30 / t_end[0], 3)
+    return out
 
 
 def c1_reference_path(oracle_c):
