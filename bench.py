@@ -291,7 +291,7 @@ def c3_records(ctx, D, gib: float, iters: int = 5):
         "physical_records_rank0": nphys,
         "bad_records": int(bad),
         "alg_GB_s_rank0": round((n + 24 * nphys) / (ms / 1e3) / 1e9, 1),
-        "path": "count (per-block header walk + header list) -> scan -> verify (production kernels)",
+        "path": "count (per-block header walk + header list) -> scan -> verify (production: v3 over blocks with <= 64 records, one lane per record over denser blocks)",
         "data": "Zipf(1.1) 64 B..32 KiB records framed on device by revel_gpu_append_records",
     }
 
