@@ -100,46 +100,71 @@ __global__ void k_reasm_emit(const revel_record_result* __restrict__ phys, uint6
     }
 }
 
-// Fragments of emitted logical records, 8 per wave visit: a fragment of at
-// most kSmallFrag bytes is copied by its own 8-lane group (small-record logs:
-// one wave per 131-B fragment left 7/8 of the wave and most of the visit idle),
-// larger ones then one after another by the whole wave.
+// Fragments of emitted logical records, 32 per wave visit, 4 per 8-lane
+// group.  Fragments of at most kTinyCopy bytes (small-record logs) are copied
+// by their group with all four fragments' loads issued before any store, so a
+// wave has 32 fragments' bytes in flight instead of 8 (the copy is latency-
+// bound: profiles/r1s3_pmc_batches_summary.txt); fragments of at most
+// kSmallFrag bytes then by their group one after another, larger ones one
+// after another by the whole wave.
 constexpr uint32_t kSmallFrag = 1024;
+constexpr uint32_t kGatherFpg = 4;  // fragments per 8-lane group and visit
 __global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image_base,
                                const revel_record_result* __restrict__ phys, uint64_t n,
                                const uint64_t* __restrict__ frag_dst, uint8_t* __restrict__ payload) {
     const uint32_t lane = lane_id(), grp = lane >> 3, gl = lane & 7u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // descriptors one visit ahead: the next visit's loads are in flight while
-    // this visit copies
-    uint64_t dst_n = w0 * 8 + grp < n ? frag_dst[w0 * 8 + grp] : ~0ull;
-    uint64_t off_n = 0;
-    uint32_t len_n = 0;
-    if (w0 * 8 + grp < n) {
-        off_n = phys[w0 * 8 + grp].file_offset;
-        len_n = phys[w0 * 8 + grp].length;
-    }
-    for (uint64_t base = w0 * 8; base < n; base += waves * 8) {
-        const uint64_t dst = dst_n;
-        const uint64_t src_off = off_n - image_base + kHeaderSize;
-        const uint32_t len = len_n;
-        const uint64_t kn = base + waves * 8 + grp;
-        dst_n = kn < n ? frag_dst[kn] : ~0ull;
-        if (kn < n) {
-            off_n = phys[kn].file_offset;
-            len_n = phys[kn].length;
+    constexpr uint64_t kVisit = 8u * kGatherFpg;
+    // descriptors one visit ahead (fragment base + 8 j + grp of a visit: each j
+    // reads 8 consecutive descriptors), clamped loads + a validity flag
+    uint64_t dst_n[kGatherFpg], off_n[kGatherFpg];
+    uint32_t len_n[kGatherFpg];
+    auto fetch = [&](uint64_t base) {
+#pragma unroll
+        for (uint32_t j = 0; j < kGatherFpg; ++j) {
+            const uint64_t k = base + 8u * j + grp;
+            const uint64_t kc = k < n ? k : n - 1;
+            const uint64_t d = frag_dst[kc];
+            dst_n[j] = k < n ? d : ~0ull;
+            off_n[j] = phys[kc].file_offset;
+            len_n[j] = phys[kc].length;
         }
-        const bool small = dst != ~0ull && len <= kSmallFrag;
-        if (small) group_copy<8>(image + src_off, payload + dst, len, gl);
-        // large fragments: one bit per group (its lane 0), whole wave each
-        uint64_t big = __ballot(dst != ~0ull && !small && gl == 0);
-        while (big) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(big);
-            big &= big - 1;
-            const uint64_t so = __shfl(src_off, l, 64), dd = __shfl(dst, l, 64);
-            const uint32_t ln = __shfl(len, l, 64);
-            group_copy<64>(image + so, payload + dd, ln, lane);
+    };
+    if (w0 * kVisit < n) fetch(w0 * kVisit);
+    for (uint64_t base = w0 * kVisit; base < n; base += waves * kVisit) {
+        uint64_t dst[kGatherFpg], src_off[kGatherFpg];
+        uint32_t len[kGatherFpg];
+#pragma unroll
+        for (uint32_t j = 0; j < kGatherFpg; ++j) {
+            dst[j] = dst_n[j];
+            src_off[j] = off_n[j] - image_base + kHeaderSize;
+            len[j] = len_n[j];
+        }
+        if (base + waves * kVisit < n) fetch(base + waves * kVisit);
+        // tiny fragments: every load of the group's four, then the stores
+        TinyCopy c[kGatherFpg];
+#pragma unroll
+        for (uint32_t j = 0; j < kGatherFpg; ++j) {
+            const bool tiny = dst[j] != ~0ull && len[j] <= kTinyCopy;
+            tiny_load(image + src_off[j], payload + (tiny ? dst[j] : 0u), tiny ? len[j] : 0u, gl, image, c[j]);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kGatherFpg; ++j)
+            if (dst[j] != ~0ull && len[j] <= kTinyCopy) tiny_store(image + src_off[j], payload + dst[j], len[j], gl, c[j]);
+#pragma unroll
+        for (uint32_t j = 0; j < kGatherFpg; ++j) {
+            const bool small = dst[j] != ~0ull && len[j] > kTinyCopy && len[j] <= kSmallFrag;
+            if (small) group_copy<8>(image + src_off[j], payload + dst[j], len[j], gl);
+            // large fragments: one bit per group (its lane 0), whole wave each
+            uint64_t big = __ballot(dst[j] != ~0ull && len[j] > kSmallFrag && gl == 0);
+            while (big) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(big);
+                big &= big - 1;
+                const uint64_t so = __shfl(src_off[j], l, 64), dd = __shfl(dst[j], l, 64);
+                const uint32_t ln = __shfl(len[j], l, 64);
+                group_copy<64>(image + so, payload + dd, ln, lane);
+            }
         }
     }
 }
@@ -167,7 +192,7 @@ hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, u
 hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
                         const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
                         hipStream_t st) {
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 31) / 32));
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 127) / 128));
     hipLaunchKernelGGL(k_reasm_gather, dim3((uint32_t)grid), dim3(256), 0, st, static_cast<const uint8_t*>(d_image),
                        image_base, d_phys, n, d_frag_dst, static_cast<uint8_t*>(d_payload));
     return hipGetLastError();

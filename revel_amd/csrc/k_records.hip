@@ -944,47 +944,77 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 
 // ---------------------------------------------------------------------------
 // Device append framing, step 1: scatter fragments (payload bytes + length
-// and type header bytes, CRC left zero) and zero the block trailers.  One
-// wave per fragment; the layout comes from the host (frame_layout()).
+// and type header bytes, CRC left zero) and zero the block trailers.  The
+// layout comes from the host (frame_layout()).
 // ---------------------------------------------------------------------------
+// FPG = fragments per 8-lane group and wave visit: 3 for small-record
+// batches, 1 when fragments average over 1 KiB (whole-wave copies then get
+// more waves instead of longer visits)
+template <uint32_t kScatterFpg>
 __global__ void k_scatter_fragments(const uint8_t* __restrict__ payloads, const revel::FragDesc* __restrict__ frags,
                                     uint64_t nfrags, uint8_t* __restrict__ image, uint64_t* __restrict__ xlist) {
-    // 8 fragments per wave visit: one of at most kSmallFragment payload bytes
-    // (or a trailer) is written by its own 8-lane group, larger ones then by
-    // the whole wave (group_copy: aligned 16-B stores)
+    // 8 FPG fragments per wave visit, FPG per 8-lane group (fragment base +
+    // 8 j + grp): payloads of at most kTinyCopy bytes are copied with all of
+    // the group's loads issued before any store (the copy is latency-bound:
+    // profiles/r1s3_pmc_batches_summary.txt), up to kSmallFragment bytes by
+    // the group one after another, larger ones by the whole wave
     constexpr uint32_t kSmallFragment = 1024;
+    constexpr uint64_t kVisit = 8u * kScatterFpg;
     const uint32_t lane = lane_id(), grp = lane >> 3, gl = lane & 7u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // descriptors one visit ahead: the next visit's load is in flight while
-    // this visit copies
-    revel::FragDesc dn{0, 0, 0, revel::kTrailer};
-    if (w0 * 8 + grp < nfrags) dn = frags[w0 * 8 + grp];
-    for (uint64_t base = w0 * 8; base < nfrags; base += waves * 8) {
-        const uint64_t f = base + grp;
-        const revel::FragDesc d = dn;
-        if (base + waves * 8 + grp < nfrags) dn = frags[base + waves * 8 + grp];
-        uint8_t* dst = image + d.dst;
-        if (f < nfrags) {
-            if (d.type == revel::kTrailer) {
-                if (gl < d.len) dst[gl] = 0;  // a trailer is < 7 bytes
-            } else if (gl < kHeaderSize) {
-                const uint32_t hv = gl < 4 ? 0u : gl == 4 ? (d.len & 0xffu) : gl == 5 ? (d.len >> 8) : d.type;
-                dst[gl] = (uint8_t)hv;
-                // header-list entry of this record for the CRC pass (CRC still 0)
-                if (gl == 0 && xlist) xlist[f] = list_entry(Hdr{0u, d.len, d.type});
-            }
+    // descriptors one visit ahead (clamped loads: no branch around a load)
+    revel::FragDesc dn[kScatterFpg];
+    auto fetch = [&](uint64_t base) {
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterFpg; ++j) {
+            const uint64_t k = base + 8u * j + grp;
+            dn[j] = frags[k < nfrags ? k : nfrags - 1];
         }
-        const bool payload = f < nfrags && d.type != revel::kTrailer;
-        const bool small = payload && d.len <= kSmallFragment;
-        if (small) group_copy<8>(payloads + d.src, dst + kHeaderSize, d.len, gl);
-        uint64_t big = __ballot(payload && !small && gl == 0);
-        while (big) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(big);
-            big &= big - 1;
-            const uint64_t so = __shfl(d.src, l, 64), dd = __shfl(d.dst, l, 64);
-            const uint32_t ln = __shfl(d.len, l, 64);
-            group_copy<64>(payloads + so, image + dd + kHeaderSize, ln, lane);
+    };
+    if (w0 * kVisit < nfrags) fetch(w0 * kVisit);
+    for (uint64_t base = w0 * kVisit; base < nfrags; base += waves * kVisit) {
+        revel::FragDesc d[kScatterFpg];
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterFpg; ++j) d[j] = dn[j];
+        if (base + waves * kVisit < nfrags) fetch(base + waves * kVisit);
+        bool live[kScatterFpg], pay[kScatterFpg];
+        TinyCopy c[kScatterFpg];
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterFpg; ++j) {
+            live[j] = base + 8u * j + grp < nfrags;
+            pay[j] = live[j] && d[j].type != revel::kTrailer;
+            const bool tiny = pay[j] && d[j].len <= kTinyCopy;
+            tiny_load(payloads + d[j].src, image + d[j].dst + kHeaderSize, tiny ? d[j].len : 0u, gl, image, c[j]);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterFpg; ++j) {
+            const uint64_t f = base + 8u * j + grp;
+            uint8_t* dst = image + d[j].dst;
+            if (live[j]) {
+                if (d[j].type == revel::kTrailer) {
+                    if (gl < d[j].len) dst[gl] = 0;  // a trailer is < 7 bytes
+                } else if (gl < kHeaderSize) {
+                    const uint32_t hv = gl < 4 ? 0u : gl == 4 ? (d[j].len & 0xffu) : gl == 5 ? (d[j].len >> 8) : d[j].type;
+                    dst[gl] = (uint8_t)hv;
+                    // header-list entry of this record for the CRC pass (CRC still 0)
+                    if (gl == 0 && xlist) xlist[f] = list_entry(Hdr{0u, d[j].len, d[j].type});
+                }
+            }
+            if (pay[j] && d[j].len <= kTinyCopy) tiny_store(payloads + d[j].src, dst + kHeaderSize, d[j].len, gl, c[j]);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterFpg; ++j) {
+            const bool small = pay[j] && d[j].len > kTinyCopy && d[j].len <= kSmallFragment;
+            if (small) group_copy<8>(payloads + d[j].src, image + d[j].dst + kHeaderSize, d[j].len, gl);
+            uint64_t big = __ballot(pay[j] && d[j].len > kSmallFragment && gl == 0);
+            while (big) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(big);
+                big &= big - 1;
+                const uint64_t so = __shfl(d[j].src, l, 64), dd = __shfl(d[j].dst, l, 64);
+                const uint32_t ln = __shfl(d[j].len, l, 64);
+                group_copy<64>(payloads + so, image + dd + kHeaderSize, ln, lane);
+            }
         }
     }
 }
@@ -1236,10 +1266,18 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
                          void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st, const uint32_t* d_counts,
                          const uint32_t* d_first, uint64_t* d_xlist) {
     if (nfrags) {
-        const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (nfrags + 31) / 32));
-        hipLaunchKernelGGL(k_scatter_fragments, dim3((uint32_t)grid), dim3(256), 0, st,
-                           static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image),
-                           d_xlist);
+        const bool small = image_len / nfrags <= 1024u;
+        const uint64_t per_wg = small ? 96 : 32;  // 4 waves x 8 groups x FPG
+        const uint64_t grid =
+            std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (nfrags + per_wg - 1) / per_wg));
+        if (small)
+            hipLaunchKernelGGL(k_scatter_fragments<3>, dim3((uint32_t)grid), dim3(256), 0, st,
+                               static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image),
+                               d_xlist);
+        else
+            hipLaunchKernelGGL(k_scatter_fragments<1>, dim3((uint32_t)grid), dim3(256), 0, st,
+                               static_cast<const uint8_t*>(d_payloads), d_frags, nfrags, static_cast<uint8_t*>(d_image),
+                               d_xlist);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
