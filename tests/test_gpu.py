@@ -637,6 +637,31 @@ def test_decode_batches_after_log_corruption(gpu_ctx):
     check_batches(gpu_ctx, bytes(img), False)  # unverified: corrupt batches decode or fail as bytes dictate
 
 
+def test_decode_batches_many_batches(gpu_ctx):
+    """9 000 small batches (35 scan tiles of the entry offsets) with malformed
+    batches spread through the log and flipped payload bits, against the
+    oracle; then a capacity cut two thirds in: infos complete, the total is
+    reported, INVALID_ARGUMENT."""
+    from tests_gen import batch_log, malformed_batches
+    rng = np.random.default_rng(45)
+    reps = batch_log(rng, 9000, max_entries=3, max_key=40, max_value=200, big_every=1501)
+    cases = [r for _, r, _ in malformed_batches()]
+    for k in range(0, len(cases) * 40, 40):
+        reps.insert(k + 7, cases[(k // 40) % len(cases)])
+    img = bytearray(oc.write_image(reps))
+    ref = oc.walk(bytes(img))
+    for v in rng.choice(len(ref), 25, replace=False):
+        if ref["length"][v] > 0:
+            img[int(ref["file_offset"][v]) + 7 + int(rng.integers(0, int(ref["length"][v])))] ^= 0x04
+    img = bytes(img)
+    infos, ents = check_batches(gpu_ctx, img)
+    assert len(infos) > 8000 and (infos["status"] != 0).sum() > 10
+    d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    out, nl, pay, pb, _ = gpu_ctx.reassemble_device(d, len(img))
+    with pytest.raises(RevelError):
+        gpu_ctx.decode_batches_device(pay, pb, out, nl, entries_cap=len(ents) * 2 // 3)
+
+
 def test_decode_batches_capacity(gpu_ctx):
     import ctypes
     from revel_amd._lib import INVALID_ARGUMENT, lib
