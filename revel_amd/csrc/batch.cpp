@@ -20,7 +20,7 @@ extern "C" int revel_gpu_decode_batches(revel_gpu_context* ctx, const void* d_pa
     if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const uint64_t n = nlogical;
-    revel::DeviceScratch S;
+    revel::DeviceScratch S(&ctx->arena);
     uint64_t *nent, *first, *tiles;
     hipError_t e = S.get(&nent, n);
     if (e == hipSuccess) e = S.get(&first, n);
@@ -34,7 +34,10 @@ extern "C" int revel_gpu_decode_batches(revel_gpu_context* ctx, const void* d_pa
     if (e == hipSuccess) e = hipMemcpyAsync(&last_first, first + n - 1, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(&last_n, nent + n - 1, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return set_error(REVEL_IO_ERROR, "decode_batches: %s", hipGetErrorString(e));
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);  // the context's scratch is free before the next call
+        return set_error(REVEL_IO_ERROR, "decode_batches: %s", hipGetErrorString(e));
+    }
     *nentries = last_first + last_n;
     if (*nentries > entries_cap)
         return set_error(REVEL_INVALID_ARGUMENT, "decode_batches: %llu entries exceed capacity %zu",

@@ -117,6 +117,7 @@ void revel_gpu_context_free(revel_gpu_context* ctx) {
     }
     if (ctx->hlist) (void)hipFree(ctx->hlist);
     if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
+    if (ctx->arena.base) (void)hipFree(ctx->arena.base);
     delete ctx;
 }
 

@@ -92,18 +92,50 @@ hipError_t batch_emit(const DeviceInfo& di, const void* d_payload, uint64_t payl
                       const revel_logical_record* d_logical, uint64_t n, const uint64_t* d_first,
                       revel_batch_info* d_info, revel_batch_entry* d_entries, uint64_t cap, hipStream_t st);
 
-// Device scratch freed when the call that allocated it returns.
+// Grow-only device scratch owned by a revel_gpu_context.  The C-ABI calls
+// that use it (decode_batches, reassemble, append framing) synchronise their
+// stream before returning, so one call's scratch is free for the next; a call
+// that fails synchronises too before it returns.
+struct ScratchArena {
+    void* base = nullptr;
+    uint64_t bytes = 0;
+    uint64_t want = 0;  // largest total a call asked for: the next call grows to it
+};
+
+// A call's scratch: carved out of the context's arena (no hipMalloc on the
+// steady path -- per-call hipMalloc/hipFree of tens of MB cost more than the
+// decode kernels); what does not fit is hipMalloc'd and freed on return, and
+// the arena grows to the whole request at the next call.
 struct DeviceScratch {
+    ScratchArena* arena;
+    uint64_t used = 0;
     void* ptrs[16] = {};
     int n = 0;
+    explicit DeviceScratch(ScratchArena* a = nullptr) : arena(a) {
+        if (arena && arena->want > arena->bytes) {
+            if (arena->base) (void)hipFree(arena->base);
+            arena->base = nullptr;
+            arena->bytes = 0;
+            if (hipMalloc(&arena->base, arena->want) == hipSuccess) arena->bytes = arena->want;
+            else arena->base = nullptr;
+        }
+    }
     ~DeviceScratch() {
         for (int i = 0; i < n; ++i) (void)hipFree(ptrs[i]);
+        if (arena && used > arena->want) arena->want = used;
     }
     template <typename T>
     hipError_t get(T** p, uint64_t count) {
+        const uint64_t bytes = ((count ? count : 1) * sizeof(T) + 255) & ~uint64_t(255);
+        const uint64_t at = used;
+        used += bytes;
+        if (arena && arena->base && used <= arena->bytes) {
+            *p = reinterpret_cast<T*>(static_cast<uint8_t*>(arena->base) + at);
+            return hipSuccess;
+        }
         void* q = nullptr;
         if (n == 16) return hipErrorOutOfMemory;
-        hipError_t e = hipMalloc(&q, (count ? count : 1) * sizeof(T));
+        hipError_t e = hipMalloc(&q, bytes);
         if (e == hipSuccess) ptrs[n++] = q;
         *p = static_cast<T*>(q);
         return e;
@@ -128,4 +160,5 @@ struct revel_gpu_context {
     const uint32_t* hlist_counts = nullptr;
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
+    revel::ScratchArena arena;  // per-call scratch of decode_batches / reassemble / append framing
 };

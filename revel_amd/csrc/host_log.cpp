@@ -412,7 +412,7 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
             if (counts[vb]++ == 0) first[vb] = (uint32_t)f;
         }
     }
-    revel::DeviceScratch scratch;
+    revel::DeviceScratch scratch(&ctx->arena);
     revel::FragDesc* d_frags = nullptr;
     uint32_t *d_counts = nullptr, *d_first = nullptr;
     uint64_t* d_xlist = nullptr;
@@ -433,7 +433,10 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
         e = revel::frame_records(ctx->di, d_payloads, d_frags, frags.size(), d_image, len, lead, st, d_counts, d_first,
                                  d_xlist);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return set_error(REVEL_IO_ERROR, "append_records: %s", hipGetErrorString(e));
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);  // the context's scratch is free before the next call
+        return set_error(REVEL_IO_ERROR, "append_records: %s", hipGetErrorString(e));
+    }
     *image_len = len;
     *block_offset = boff;
     return REVEL_OK;

@@ -22,7 +22,7 @@ extern "C" int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image,
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const uint64_t n = nphys;
     const uint64_t tiles = revel::scan_scratch_words(n);
-    revel::DeviceScratch S;
+    revel::DeviceScratch S(&ctx->arena);
     uint32_t *flag, *end, *idx, *t32;
     uint64_t *len, *off, *dst, *t64;
     hipError_t e = hipSuccess;
@@ -49,7 +49,10 @@ extern "C" int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image,
     if (e == hipSuccess) e = hipMemcpyAsync(&last_off, off + n - 1, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(&last_len, len + n - 1, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return set_error(REVEL_IO_ERROR, "reassemble: %s", hipGetErrorString(e));
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);  // the context's scratch is free before the next call
+        return set_error(REVEL_IO_ERROR, "reassemble: %s", hipGetErrorString(e));
+    }
     *nlogical = (uint64_t)last_idx + last_flag;
     *payload_bytes = last_off + last_len;
     return REVEL_OK;
