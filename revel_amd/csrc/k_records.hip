@@ -676,7 +676,40 @@ struct BlockSeq {
 // ---------------------------------------------------------------------------
 enum BlockSel : int { SEL_ALL = 0, SEL_DENSE = 1, SEL_SPARSE = 2 };
 
-template <bool FRAME, int SEL = SEL_ALL>
+// TQ (variant 9 experiment): round loads coalesced per quad -- lane 4q+p loads
+// 16-B piece p of each 64-B half of the four chunks 4q..4q+3 (16 TCP accesses
+// per wave instruction instead of 64) -- and a 4x4 transpose of the 16-B
+// pieces inside the quad (two DPP butterfly stages) hands every lane its own
+// chunk's bytes, so the per-lane CRC logic is unchanged.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_qperm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int K, int CTRL>
+__device__ __forceinline__ void quad_stage(uint4* v, bool bit) {
+#pragma unroll
+    for (int h = 0; h < 1; ++h) {
+#pragma unroll
+        for (int r0 = 0; r0 < 4; ++r0) {
+            if (r0 & K) continue;
+            uint32_t* a = reinterpret_cast<uint32_t*>(&v[4 * h + r0]);
+            uint32_t* b = reinterpret_cast<uint32_t*>(&v[4 * h + (r0 | K)]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                // bit clear: keep a, b <- partner's a; bit set: keep b, a <- partner's b
+                const uint32_t recv = dpp_qperm<CTRL>(bit ? a[c] : b[c]);
+                a[c] = bit ? recv : a[c];
+                b[c] = bit ? b[c] : recv;
+            }
+        }
+    }
+}
+__device__ __forceinline__ void quad_transpose(uint4* v, uint32_t lane) {
+    quad_stage<1, 0xB1>(v, (lane & 1u) != 0);  // quad_perm [1,0,3,2]
+    quad_stage<2, 0x4E>(v, (lane & 2u) != 0);  // quad_perm [2,3,0,1]
+}
+
+template <bool FRAME, int SEL = SEL_ALL, bool TQ = false, bool R64 = false>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -713,13 +746,22 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     BlockSeq<SEL == SEL_DENSE> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg);
     uint64_t b = SEL != SEL_ALL ? seq.next(counts, nwaves, b_hi) : b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
     if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
+    constexpr int kRoundLoads = (TQ || R64) ? 4 : 8, kRounds = 32 / kRoundLoads;  // 16-B loads per round, rounds per chunk
     uint4 cur[8], nxt[8];
     uint32_t pf_count = kNone, pf_first = 0;
     uint64_t pf_hl = 0;
     auto load_round = [&](const uint8_t* blk, uint4* v, int rr, bool own, uint32_t cs_ref) {
-        const uint8_t* p = blk + (own ? cs : cs_ref) + rr * 128;
+        if constexpr (TQ) {
+            // every lane loads for its quad (own / cs_ref unused: all chunks read)
+            // 64-B rounds: the quad transpose needs registers the 128-B rounds do not have
+            const uint8_t* p = blk + (lane & ~3u) * 512u + rr * 64 + (lane & 3u) * 16u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 16));
+            for (int j = 0; j < 4; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 512));
+        } else {
+            const uint8_t* p = blk + (own ? cs : cs_ref) + rr * (16 * kRoundLoads);
+#pragma unroll
+            for (int j = 0; j < kRoundLoads; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 16));
+        }
     };
     // header list first: the list is needed before the data (loads return in order)
     auto prefetch = [&](uint64_t nb) {
@@ -833,12 +875,13 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                 const uint32_t cs_ref = (uint32_t)__builtin_ctzll(act_mask) * 512u;  // wave-uniform
                 if (!have_round0) load_round(blk, cur, 0, active, cs_ref);
 #pragma unroll 1
-                for (int rr = 0; rr < 4; ++rr) {
-                    if (rr < 3) load_round(blk, nxt, rr + 1, active, cs_ref);
+                for (int rr = 0; rr < kRounds; ++rr) {
+                    if (rr < kRounds - 1) load_round(blk, nxt, rr + 1, active, cs_ref);
                     __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (TQ) quad_transpose(cur, lane);
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const uint32_t p16 = cs + rr * 128 + j * 16;
+                    for (int j = 0; j < kRoundLoads; ++j) {
+                        const uint32_t p16 = cs + rr * (16 * kRoundLoads) + j * 16;
                         // don't-care bytes before the next record, or inside one
                         const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
                         if (__all(interior)) {
@@ -880,7 +923,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                     }
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+                    for (int j = 0; j < kRoundLoads; ++j) cur[j] = nxt[j];
                 }
                 // record still open at the chunk end: shift its partial register to e
                 if (r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(g_x8n_tab[e - ce], state));
@@ -1135,7 +1178,7 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
 // sparse partial blocks through the single-wave verify2 launch.  Each kernel
 // skips the others' blocks by count.  Lists: verify = hlist + overflow entries
 // in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
-template <bool FRAME, bool SPARSE_V5 = false>
+template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
@@ -1151,7 +1194,7 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
             hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(b_hi, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
                                nbytes, base_offset, d_first, d_out, hl, d_counts);
         } else {
-            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
+            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE, TQ, R64>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
                                d_counts, xl, xs);
         }
@@ -1228,6 +1271,16 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return launch_verify_split<false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
                                                     reinterpret_cast<const uint64_t*>(d_out),
                                                     (uint32_t)(sizeof(revel_record_result) / 8), st);
+        case 9:  // experiment: split with quad-coalesced loads + DPP transpose in v3
+            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
+            return launch_verify_split<false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                           d_counts, reinterpret_cast<const uint64_t*>(d_out),
+                                                           (uint32_t)(sizeof(revel_record_result) / 8), st);
+        case 10:  // control for 9: the same 64-B rounds with lane-owned loads
+            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
+            return launch_verify_split<false, false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                                  d_counts, reinterpret_cast<const uint64_t*>(d_out),
+                                                                  (uint32_t)(sizeof(revel_record_result) / 8), st);
         case 0:
             if (hl && d_counts && aligned16(img))
                 return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
