@@ -982,6 +982,211 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     }
 }
 
+// ---------------------------------------------------------------------------
+// C3 sparse verify, ring experiment (variant 11): v3's per-lane logic over the
+// blocks with at most kListPerBlock records, with the two 128-B rounds as a
+// 16-slot register ring -- a slot is refilled the moment it is consumed, with
+// the data two rounds ahead (this block's rounds 2, 3, then the NEXT block's
+// rounds 0, 1), so ~15 of 16 slots stay in flight across block boundaries
+// instead of v3's one round issued per round.  Same registers, same 16 waves/CU.
+// The next block's list entry / count / output slot are issued before its data.
+// ---------------------------------------------------------------------------
+template <int kRingGroup>
+__global__ __launch_bounds__(kVerify2Threads) void k_verify_records3r(const uint8_t* __restrict__ image,
+                                                                      uint64_t nbytes, uint64_t base_offset,
+                                                                      const uint32_t* __restrict__ first,
+                                                                      revel_record_result* __restrict__ out,
+                                                                      uint32_t lead,
+                                                                      const uint64_t* __restrict__ hlist,
+                                                                      const uint32_t* __restrict__ counts) {
+    __shared__ uint32_t tab[32768];
+    __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
+    fill_tables<TM_S4R>(tab);
+    __syncthreads();
+    VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
+    const LaneConst L = make_lane_const();
+    const uint32_t lane = lane_id();
+    const uint64_t vbytes = nbytes + lead;
+    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;
+    const uint64_t waves_per_wg = kVerify2Threads / 64;
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    const uint32_t cs = lane * 512u, ce = cs + 512u;
+    const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    BlockSeq<false> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg);
+    uint64_t b = seq.next(counts, nwaves, b_hi);
+    if (b >= b_hi) return;  // wave-uniform
+    uint32_t pf_count = counts[b], pf_first = first[b];
+    // list row base in SGPRs + a 32-bit lane offset (saddr form): a per-lane
+    // 64-bit row pointer held across the loop spilled, and its reload drained the ring
+    auto list_entry_of = [&](uint64_t blk_idx) {
+        const uint64_t* row = hlist + blk_idx * kListStride;
+        uint32_t lo = lane * 8u;
+        asm volatile("" : "+v"(lo));  // keep the compiler from hoisting a 64-bit row + lane pointer
+        return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(row) + lo);
+    };
+    uint64_t pf_hl = list_entry_of(b);
+    uint4 A[8], B[8];
+    // slots refilled together: the group's loads hit the same lane line back to
+    // back (one refill per slot spread a line's 8 accesses over a round, and
+    // with 128 KiB of lines in flight per CU the line left the L1 in between)
+    auto load8 = [&](uint4* v, const uint8_t* p) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 16));
+    };
+    {
+        const uint8_t* blk0 = image + b * kBlockSize - lead;
+        load8(A, blk0 + cs);
+        load8(B, blk0 + cs + 128);
+    }
+    while (b < b_hi) {
+        const uint64_t base = b * kBlockSize;
+        const uint8_t* blk = image + base - lead;
+        const uint64_t bn = seq.next(counts, nwaves, b_hi);
+        const uint8_t* nblk = bn < b_hi ? image + bn * kBlockSize - lead : blk;  // loads stay unconditional
+        const uint32_t np = min(pf_count, kListPerBlock);
+        const uint32_t out_base = __builtin_amdgcn_readfirstlane(pf_first);
+        {
+            const Hdr h = list_header(pf_hl);
+            const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
+            const uint32_t off = wave_exclusive_sum(sz);
+            if (lane < np) {
+                const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
+                wl.off[lane] = (uint16_t)off;
+                wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
+                wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
+                wl.acc[lane] = 0;
+                wl.hstored[lane] = h.stored;
+                wl.hlt[lane] = h.len | (h.type << 16);
+            }
+            if (lane == 0) wl.s[np] = wl.em1[np] = kNoRange;
+        }
+        wave_lds_sync();
+        const uint32_t nrec = np;
+        uint32_t lo = 0, hi = nrec;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
+        }
+        uint32_t r = lo, s = wl.s[r], e = uint32_t(wl.em1[r]) + 1u;
+        // the finalizer's table lookups are issued here, behind this block's
+        // rounds 0, 1 and ahead of every refill: issued after the refills,
+        // waiting for them would drain the ring
+        uint32_t xo;  // x^(8(e - ce)) of the record open at the chunk end (if any)
+        {
+            lo = r, hi = nrec;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (uint32_t(wl.em1[mid]) + 1u > ce) hi = mid; else lo = mid + 1;
+            }
+            const uint32_t so = wl.s[lo], eo = uint32_t(wl.em1[lo]) + 1u;
+            const bool open = lo < nrec && so < ce && eo > ce;
+            xo = g_x8n_tab[open ? eo - ce : 0u];
+        }
+        // (a bad header's length can exceed the table: only in-block lengths index it)
+        const uint32_t ln = lane < nrec ? wl.hlt[lane] & 0xFFFFu : kBlockSize;
+        const uint32_t ix = g_init_xor_tab[ln < kBlockSize ? ln + 1u : 0u];
+        uint32_t state = 0;
+        auto consume = [&](const uint4 v, const uint32_t p16) {
+            const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
+            if (__all(interior)) {
+                state = p16 == s ? 0u : state;
+                state = absorb4<TM_S4R>(state, v, L, tab);
+            } else {
+                // rolled: 32 slots are unrolled, the boundary path is kept small
+#pragma unroll 1
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t p = p16 + q * 4u;
+                    const uint32_t w = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+                    if (s >= p + 4u) {
+                    } else if (e > p + 4u) {
+                        if (s >= p) state = 0;
+                        const uint32_t lb = s > p ? s - p : 0u;
+                        state = absorb<TM_S4R>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
+                    } else if (e > p) {
+                        if (s >= p) state = 0;
+                        const uint32_t lb = s > p ? s - p : 0u;
+                        const uint32_t hb = e - p;
+                        if (lb == 0 && hb == 4) {
+                            state = absorb<TM_S4R>(state, w, L, tab);
+                        } else {
+                            for (uint32_t t = lb; t < hb; ++t)
+                                state = byte_step_s4r(state, (w >> (8u * t)) & 0xffu, L, tab);
+                        }
+                        atomicXor(&wl.acc[r], state);
+                        state = 0;
+                        ++r;
+                        s = wl.s[r];
+                        e = uint32_t(wl.em1[r]) + 1u;
+                    }
+                }
+            }
+        };
+        // rounds 0, 1 of this block are in A, B; each consumed slot is refilled
+        // two rounds ahead
+#pragma unroll
+        for (int g = 0; g < 8; g += kRingGroup) {
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j) consume(A[j], cs + j * 16);
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j)
+                A[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + 256 + j * 16));
+        }
+#pragma unroll
+        for (int g = 0; g < 8; g += kRingGroup) {
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j) consume(B[j], cs + 128 + j * 16);
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j)
+                B[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + 384 + j * 16));
+        }
+        // the next block's list before its data (loads complete in order)
+        if (bn < b_hi) {
+            pf_count = counts[bn];
+            pf_first = first[bn];
+            pf_hl = list_entry_of(bn);
+        }
+#pragma unroll
+        for (int g = 0; g < 8; g += kRingGroup) {
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j) consume(A[j], cs + 256 + j * 16);
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j)
+                A[j] = ldg4_plain(reinterpret_cast<const uint4*>(nblk + cs + j * 16));
+        }
+#pragma unroll
+        for (int g = 0; g < 8; g += kRingGroup) {
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j) consume(B[j], cs + 384 + j * 16);
+#pragma unroll
+            for (int j = g; j < g + kRingGroup; ++j)
+                B[j] = ldg4_plain(reinterpret_cast<const uint4*>(nblk + cs + 128 + j * 16));
+        }
+        if (r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(xo, state));
+        wave_lds_sync();
+        if (lane < nrec) {
+            const uint32_t off = wl.off[lane];
+            const Hdr h{wl.hstored[lane], wl.hlt[lane] & 0xFFFFu, wl.hlt[lane] >> 16};
+            const uint32_t st = classify(h, off, kBlockSize);
+            revel_record_result res;
+            res.file_offset = base_offset + base - lead + off;
+            res.length = h.len;
+            res.stored_crc = h.stored;
+            res.type = (uint8_t)h.type;
+            res.reserved[0] = res.reserved[1] = 0;
+            if (st == REVEL_REC_OK) {
+                res.computed_crc = mask(wl.acc[lane] ^ ix);
+                res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
+            } else {
+                res.computed_crc = 0;
+                res.status = (uint8_t)st;
+            }
+            out[out_base + lane] = res;
+        }
+        wave_lds_sync();
+        b = bn;
+    }
+}
+
 #include "verify5.inc"
 #include "verify_dense.inc"
 
@@ -1178,7 +1383,7 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
 // sparse partial blocks through the single-wave verify2 launch.  Each kernel
 // skips the others' blocks by count.  Lists: verify = hlist + overflow entries
 // in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
-template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false>
+template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false, int RING = 0>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
@@ -1193,6 +1398,11 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
             static_assert(!FRAME, "v5 verifies only");
             hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(b_hi, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
                                nbytes, base_offset, d_first, d_out, hl, d_counts);
+        } else if constexpr (RING != 0) {
+            static_assert(!FRAME, "ring experiment verifies only");
+            hipLaunchKernelGGL(k_verify_records3r<RING>, dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
+                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
+                               d_counts);
         } else {
             hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE, TQ, R64>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
@@ -1281,6 +1491,21 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return launch_verify_split<false, false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
                                                                   d_counts, reinterpret_cast<const uint64_t*>(d_out),
                                                                   (uint32_t)(sizeof(revel_record_result) / 8), st);
+        case 11:  // experiments: sparse blocks through the 16-slot ring kernel,
+        case 12:  // slots refilled in groups of 4 (11), 8 (12), 2 (13)
+        case 13: {
+            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
+            const uint64_t* xl = reinterpret_cast<const uint64_t*>(d_out);
+            const uint32_t xs = (uint32_t)(sizeof(revel_record_result) / 8);
+            if (variant == 11)
+                return launch_verify_split<false, false, false, false, 4>(di, img, nbytes, base_offset, d_first,
+                                                                          d_out, 0u, hl, d_counts, xl, xs, st);
+            if (variant == 12)
+                return launch_verify_split<false, false, false, false, 8>(di, img, nbytes, base_offset, d_first,
+                                                                          d_out, 0u, hl, d_counts, xl, xs, st);
+            return launch_verify_split<false, false, false, false, 2>(di, img, nbytes, base_offset, d_first, d_out,
+                                                                      0u, hl, d_counts, xl, xs, st);
+        }
         case 0:
             if (hl && d_counts && aligned16(img))
                 return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,

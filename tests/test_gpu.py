@@ -124,7 +124,7 @@ def compare_walk(res, ref):
         assert np.array_equal(res[f].astype(np.uint64), ref[f].astype(np.uint64)), f
 
 
-VERIFY_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]
+VERIFY_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13]
 
 
 @pytest.mark.parametrize("variant", VERIFY_VARIANTS)
@@ -286,7 +286,7 @@ def test_verify_mixed_density(gpu_ctx, tail):
     ref = oc.walk(img)
     assert (ref["status"] == 1).sum() > 10
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    for v in (0, 7, 8, 9):
+    for v in (0, 7, 8, 9, 11):
         compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref)
 
 
