@@ -685,10 +685,10 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_qperm(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
-template <int K, int CTRL>
+template <int K, int CTRL, int H = 1>
 __device__ __forceinline__ void quad_stage(uint4* v, bool bit) {
 #pragma unroll
-    for (int h = 0; h < 1; ++h) {
+    for (int h = 0; h < H; ++h) {
 #pragma unroll
         for (int r0 = 0; r0 < 4; ++r0) {
             if (r0 & K) continue;
@@ -704,12 +704,13 @@ __device__ __forceinline__ void quad_stage(uint4* v, bool bit) {
         }
     }
 }
+template <int H = 1>
 __device__ __forceinline__ void quad_transpose(uint4* v, uint32_t lane) {
-    quad_stage<1, 0xB1>(v, (lane & 1u) != 0);  // quad_perm [1,0,3,2]
-    quad_stage<2, 0x4E>(v, (lane & 2u) != 0);  // quad_perm [2,3,0,1]
+    quad_stage<1, 0xB1, H>(v, (lane & 1u) != 0);  // quad_perm [1,0,3,2]
+    quad_stage<2, 0x4E, H>(v, (lane & 2u) != 0);  // quad_perm [2,3,0,1]
 }
 
-template <bool FRAME, int SEL = SEL_ALL, bool TQ = false, bool R64 = false>
+template <bool FRAME, int SEL = SEL_ALL, bool TQ = false, bool R64 = false, bool TQ8 = false>
 __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                                      uint64_t base_offset,
                                                                      const uint32_t* __restrict__ first,
@@ -746,12 +747,20 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     BlockSeq<SEL == SEL_DENSE> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg);
     uint64_t b = SEL != SEL_ALL ? seq.next(counts, nwaves, b_hi) : b_lo + blockIdx.x * waves_per_wg + wave_in_wg;
     if (b >= b_hi) return;  // wave-uniform; no workgroup barrier follows
-    constexpr int kRoundLoads = (TQ || R64) ? 4 : 8, kRounds = 32 / kRoundLoads;  // 16-B loads per round, rounds per chunk
+    constexpr int kRoundLoads = ((TQ && !TQ8) || R64) ? 4 : 8, kRounds = 32 / kRoundLoads;  // 16-B loads per round, rounds per chunk
     uint4 cur[8], nxt[8];
     uint32_t pf_count = kNone, pf_first = 0;
     uint64_t pf_hl = 0;
     auto load_round = [&](const uint8_t* blk, uint4* v, int rr, bool own, uint32_t cs_ref) {
-        if constexpr (TQ) {
+        if constexpr (TQ && TQ8) {
+            // 128-B rounds: lane 4q+p loads piece p of each 64-B half of chunks 4q..4q+3
+            const uint8_t* p = blk + (lane & ~3u) * 512u + rr * 128 + (lane & 3u) * 16u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    v[4 * h + j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 512 + h * 64));
+        } else if constexpr (TQ) {
             // every lane loads for its quad (own / cs_ref unused: all chunks read)
             // 64-B rounds: the quad transpose needs registers the 128-B rounds do not have
             const uint8_t* p = blk + (lane & ~3u) * 512u + rr * 64 + (lane & 3u) * 16u;
@@ -876,9 +885,15 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
                 if (!have_round0) load_round(blk, cur, 0, active, cs_ref);
 #pragma unroll 1
                 for (int rr = 0; rr < kRounds; ++rr) {
+                    // TQ8: transpose before the next round is issued (its 32 registers
+                    // are not live yet: the transpose's temporaries fit)
+                    if constexpr (TQ && TQ8) {
+                        quad_transpose<2>(cur, lane);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                     if (rr < kRounds - 1) load_round(blk, nxt, rr + 1, active, cs_ref);
                     __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (TQ) quad_transpose(cur, lane);
+                    if constexpr (TQ && !TQ8) quad_transpose(cur, lane);
 #pragma unroll
                     for (int j = 0; j < kRoundLoads; ++j) {
                         const uint32_t p16 = cs + rr * (16 * kRoundLoads) + j * 16;
@@ -1383,7 +1398,7 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
 // sparse partial blocks through the single-wave verify2 launch.  Each kernel
 // skips the others' blocks by count.  Lists: verify = hlist + overflow entries
 // in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
-template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false, int RING = 0>
+template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false, int RING = 0, bool TQ8 = false>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
@@ -1404,7 +1419,7 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
                                d_counts);
         } else {
-            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE, TQ, R64>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
+            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE, TQ, R64, TQ8>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
                                d_counts, xl, xs);
         }
@@ -1491,6 +1506,11 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return launch_verify_split<false, false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
                                                                   d_counts, reinterpret_cast<const uint64_t*>(d_out),
                                                                   (uint32_t)(sizeof(revel_record_result) / 8), st);
+        case 14:  // experiment: variant 9's quad transpose with 128-B rounds
+            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
+            return launch_verify_split<false, false, true, false, 0, true>(
+                di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                reinterpret_cast<const uint64_t*>(d_out), (uint32_t)(sizeof(revel_record_result) / 8), st);
         case 11:  // experiments: sparse blocks through the 16-slot ring kernel,
         case 12:  // slots refilled in groups of 4 (11), 8 (12), 2 (13)
         case 13: {

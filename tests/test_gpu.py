@@ -124,7 +124,7 @@ def compare_walk(res, ref):
         assert np.array_equal(res[f].astype(np.uint64), ref[f].astype(np.uint64)), f
 
 
-VERIFY_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13]
+VERIFY_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14]
 
 
 @pytest.mark.parametrize("variant", VERIFY_VARIANTS)
