@@ -3,6 +3,8 @@
 Config C2 (full-type blocks), config C3 (variable records via the device
 walk + segmented CRC), the GPU-verified Reader, and size-independent
 properties at larger sizes."""
+import os
+
 import numpy as np
 import pytest
 
@@ -799,3 +801,19 @@ def test_property_batch_decode_mutations(gpu_ctx):
         check_batches(gpu_ctx, oc.write_image([bytes(r) for r in reps]))
 
     prop()
+
+
+@pytest.mark.gpu
+def test_c1_native_cabi_roundtrip():
+    """Config C1 through the C-ABI from a native caller (tools/c1_native.cpp,
+    built by __graft_entry__.build()): 10 000 x 4 KiB records appended and read
+    back with checksum=1; the binary exits non-zero unless every record
+    matches and the image is the 41 038 750-B image of SURVEY 8(a) a9."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "c1_native")
+    assert os.path.exists(exe), "tools/c1_native not built (run __graft_entry__.build())"
+    p = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    out = json.loads(p.stdout)
+    assert out["records_equal"] and out["image_bytes"] == 41038750
