@@ -118,6 +118,12 @@ void revel_gpu_context_free(revel_gpu_context* ctx) {
     if (ctx->hlist) (void)hipFree(ctx->hlist);
     if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
     if (ctx->arena.base) (void)hipFree(ctx->arena.base);
+    auto& pr = ctx->parked_reader;
+    if (pr.h_win) (void)hipHostFree(pr.h_win);
+    if (pr.d_win) (void)hipFree(pr.d_win);
+    if (pr.d_counts) (void)hipFree(pr.d_counts);
+    if (pr.d_first) (void)hipFree(pr.d_first);
+    if (pr.d_out) (void)hipFree(pr.d_out);
     delete ctx;
 }
 

@@ -161,4 +161,16 @@ struct revel_gpu_context {
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
     revel::ScratchArena arena;  // per-call scratch of decode_batches / reassemble / append framing
+    // Window buffers of the last revel_log_reader freed on this context, parked
+    // for the next reader with the same window (host_log.cpp): a reader per log
+    // file no longer pays a pinned + device allocation of the window each time.
+    struct ParkedReader {
+        size_t window = 0;
+        uint8_t* h_win = nullptr;  // pinned
+        void* d_win = nullptr;
+        uint32_t* d_counts = nullptr;
+        uint32_t* d_first = nullptr;
+        revel_record_result* d_out = nullptr;
+        size_t d_out_cap = 0;
+    } parked_reader;
 };

@@ -565,6 +565,23 @@ int load_window(revel_log_reader* r) {
 }
 
 void reader_release(revel_log_reader* r) {
+    if (r->gpu && r->win && r->d_win && r->d_counts && r->d_first) {
+        auto& pr = r->gpu->parked_reader;
+        if (!pr.h_win) {  // park the window buffers for the next reader on this context
+            pr.window = r->window;
+            pr.h_win = r->win;
+            pr.d_win = r->d_win;
+            pr.d_counts = r->d_counts;
+            pr.d_first = r->d_first;
+            pr.d_out = r->d_out;
+            pr.d_out_cap = r->d_out_cap;
+            r->win = nullptr;
+            r->d_win = nullptr;
+            r->d_counts = r->d_first = nullptr;
+            r->d_out = nullptr;
+            r->d_out_cap = 0;
+        }
+    }
     if (r->gpu) {
         if (r->win) revel_gpu_host_free(r->gpu, r->win);
         revel_gpu_free(r->gpu, r->d_win);
@@ -602,7 +619,16 @@ int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t ini
     r->window = (w + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE * REVEL_BLOCK_SIZE;
     const size_t nblocks = r->window / REVEL_BLOCK_SIZE;
     int rc = REVEL_OK;
-    if (gpu) {
+    if (gpu && gpu->parked_reader.h_win && gpu->parked_reader.window == r->window) {
+        auto& pr = gpu->parked_reader;  // the previous reader's buffers (same window)
+        r->win = pr.h_win;
+        r->d_win = pr.d_win;
+        r->d_counts = pr.d_counts;
+        r->d_first = pr.d_first;
+        r->d_out = pr.d_out;
+        r->d_out_cap = pr.d_out_cap;
+        pr = revel_gpu_context::ParkedReader{};
+    } else if (gpu) {
         rc = revel_gpu_host_alloc(gpu, r->window, reinterpret_cast<void**>(&r->win));
         if (!rc) rc = revel_gpu_malloc(gpu, r->window, &r->d_win);
         if (!rc) rc = revel_gpu_malloc(gpu, nblocks * 4, reinterpret_cast<void**>(&r->d_counts));

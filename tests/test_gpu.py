@@ -817,3 +817,37 @@ def test_c1_native_cabi_roundtrip():
     assert p.returncode == 0, p.stderr
     out = json.loads(p.stdout)
     assert out["records_equal"] and out["image_bytes"] == 41038750
+
+
+@pytest.mark.gpu
+def test_reader_parked_window_buffers(gpu_ctx, golden_index):
+    """Readers on one context reuse the window buffers the previous reader
+    parked on it (same window size): sequential readers, overlapping readers
+    (the second allocates its own) and a different window size all read every
+    golden image exactly as the oracle reader does."""
+    names = sorted(golden_index)
+    want = {}
+    for name in names:
+        try:
+            want[name] = po.read_all(golden_image(name), checksum=True)
+        except po.CorruptionError:
+            want[name] = "error"
+
+    def read(rd):
+        try:
+            return list(rd)
+        except RevelError as e:
+            assert e.code == IO_ERROR
+            return "error"
+
+    for window in (65536, 65536, 1 << 20, 65536):
+        for a, b in zip(names, names[1:] + names[:1]):
+            ra = log.Reader(env.MemorySequentialFile(golden_image(a)), checksum=True, gpu=gpu_ctx, window_bytes=window)
+            rb = log.Reader(env.MemorySequentialFile(golden_image(b)), checksum=True, gpu=gpu_ctx, window_bytes=window)
+            assert read(rb) == want[b], (b, window)
+            assert read(ra) == want[a], (a, window)
+            del ra  # parks its buffers; rb's are freed (slot taken)
+            del rb
+            rc = log.Reader(env.MemorySequentialFile(golden_image(a)), checksum=True, gpu=gpu_ctx, window_bytes=window)
+            assert read(rc) == want[a], (a, window)
+            del rc
