@@ -125,9 +125,32 @@ SIGNATURES = {
 EXTRA_SIGNATURES = {
     "revel_gpu_verify_records_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
                                                  c_void_p, c_void_p]),
-    "revel_gpu_crc_full_blocks_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p,
-                                                  c_void_p]),
 }
+
+# tools/experiments/libexperiments.so: kernel variants kept for the record
+EXPERIMENT_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "experiments",
+                               "libexperiments.so")
+EXPERIMENT_SIGNATURES = {
+    "revel_x_crc_full_blocks_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p,
+                                                c_void_p]),
+}
+_xlib = None
+
+
+def experiments() -> ctypes.CDLL:
+    """The experiment library (built by `make -C tools/experiments`); the
+    product never loads it."""
+    global _xlib
+    if _xlib is None:
+        if not os.path.exists(EXPERIMENT_PATH):
+            raise RuntimeError(f"{EXPERIMENT_PATH} is missing: `make -C tools/experiments`")
+        L = ctypes.CDLL(EXPERIMENT_PATH)
+        for name, (res, args) in EXPERIMENT_SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _xlib = L
+    return _xlib
 
 _lib = None
 

@@ -134,20 +134,8 @@ int revel_gpu_crc_full_blocks(revel_gpu_context* ctx, const void* d_blocks, size
     CHECK_CTX(ctx);
     if (nblocks == 0) return REVEL_OK;
     if (!d_blocks || !d_masked_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    HIP_TRY(revel::crc_full_blocks_variant(ctx->di, 0, d_blocks, nblocks, d_masked_out, d_ok, pick(ctx, stream)),
+    HIP_TRY(revel::crc_full_blocks(ctx->di, d_blocks, nblocks, d_masked_out, d_ok, pick(ctx, stream)),
             "crc_full_blocks launch");
-    return REVEL_OK;
-}
-
-// Experiment hook (not in the public header): same contract as
-// revel_gpu_crc_full_blocks for a given kernel variant.
-int revel_gpu_crc_full_blocks_variant(revel_gpu_context* ctx, int variant, const void* d_blocks, size_t nblocks,
-                                      uint32_t* d_masked_out, uint8_t* d_ok, void* stream) {
-    CHECK_CTX(ctx);
-    if (nblocks == 0) return REVEL_OK;
-    if (!d_blocks || !d_masked_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    HIP_TRY(revel::crc_full_blocks_variant(ctx->di, variant, d_blocks, nblocks, d_masked_out, d_ok, pick(ctx, stream)),
-            "crc_full_blocks_variant launch");
     return REVEL_OK;
 }
 
@@ -178,7 +166,7 @@ int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t 
         if (ctx->hlist) (void)hipFree(ctx->hlist);
         ctx->hlist = nullptr;
         ctx->hlist_cap_blocks = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->hlist), nblocks * revel::kListStride * sizeof(uint64_t)),
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->hlist), revel::hlist_words(nblocks) * sizeof(uint64_t)),
                 "hipMalloc(header list)");
         ctx->hlist_cap_blocks = nblocks;
     }

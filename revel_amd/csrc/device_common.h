@@ -217,6 +217,75 @@ __device__ __forceinline__ uint32_t step_x(uint32_t x, uint32_t wn, LaneConst L,
     return xor3(xor3(ldsw<0>(tab, a0), ldsw<128>(tab, a1), ldsw<0>(tab, a2)), ldsw<128>(tab, a3), wn);
 }
 
+// ---------------------------------------------------------------------------
+// Interleaved word streams with the gap folded into the tables (C2 k_full_blocks4,
+// C3 k_verify_rows).  A stream is the 32-bit words of a block at a fixed offset
+// within every row of ROW bytes; consecutive words of a stream are ROW bytes
+// apart, so with T''m = x^(8*(ROW-4)) * Tm one x-state step
+//     U <- T''3[x0] ^ T''2[x1] ^ T''1[x2] ^ T''0[x3],   x = U ^ w
+// absorbs a word AND the ROW-4 bytes of other streams that follow it (shifting
+// is linear, so it distributes over the table xor): T''(v) = v * x^(8*ROW).
+// ---------------------------------------------------------------------------
+struct GapTables {
+    uint32_t t[4][256];  // t[m][e] = x^(8*gap) * T_m[e]
+};
+constexpr GapTables make_gap_tables(uint32_t gap) {
+    GapTables g{};
+    const SliceTables st = make_slice_tables();
+    const uint32_t c = x8n(gap);
+    for (int m = 0; m < 4; ++m)
+        for (int e = 0; e < 256; ++e) g.t[m][e] = multmodp(c, st.t[m][e]);
+    return g;
+}
+__constant__ GapTables c_gap1020 = make_gap_tables(1020);  // 1 KiB rows (C2)
+__constant__ GapTables c_gap252 = make_gap_tables(252);    // 256-B rows (C3)
+
+constexpr uint32_t pow_modp(uint32_t a, uint64_t n) {
+    uint32_t r = 0x80000000u;
+    while (n) {
+        if (n & 1u) r = multmodp(r, a);
+        a = multmodp(a, a);
+        n >>= 1;
+    }
+    return r;
+}
+constexpr uint32_t kXInv = 0x05EC76F1u;  // x^-1 mod P, reflected (P(0) = 1, so x is invertible)
+static_assert(multmodp(kXInv, 0x40000000u) == 0x80000000u, "x * x^-1 == 1");
+// x^(-8 * 4 * 2^L): tree level L combines streams 2^L apart (4 * 2^L bytes)
+struct InvTreeConsts {
+    uint32_t c[8];
+};
+constexpr InvTreeConsts make_inv_tree() {
+    InvTreeConsts t{};
+    for (int L = 0; L < 8; ++L) t.c[L] = pow_modp(kXInv, 8ull * 4ull * (1ull << L));
+    return t;
+}
+__constant__ InvTreeConsts c_inv_tree = make_inv_tree();
+static_assert(multmodp(make_inv_tree().c[0], x8n(4)) == 0x80000000u, "inverse shift");
+
+// S4R image of a gap table set (128 KiB, replicated 32x):
+// byte0 -> T''3 (r0 h0), byte1 -> T''2 (r0 h1), byte2 -> T''1 (r1 h0), byte3 -> T''0 (r1 h1)
+__device__ void fill_gap_tables(uint32_t* tab, const GapTables& g) {
+    for (uint32_t d = threadIdx.x; d < 32768u; d += blockDim.x) {
+        const uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
+        tab[d] = g.t[3 - (r * 2 + h)][e];
+    }
+}
+// Inverse-shift tables, `levels` x 4 KiB unreplicated: level L, byte k, entry e at
+// shtab[L*1024 + k*256 + e] = (e << 8k) * x^(-32 * 2^L) mod P.
+__device__ void fill_inv_tree_tables(uint32_t* shtab, int levels) {
+    for (uint32_t d = threadIdx.x; d < uint32_t(levels) * 1024u; d += blockDim.x) {
+        const uint32_t L = d >> 10, k = (d >> 8) & 3u, e = d & 255u;
+        shtab[d] = gf_mul(c_inv_tree.c[L], e << (8u * k));
+    }
+}
+// v * (the level-L constant of shtab), four unreplicated lookups.
+template <int L>
+__device__ __forceinline__ uint32_t tree_shift(const uint32_t* shtab, uint32_t v) {
+    const uint32_t* t = shtab + L * 1024;
+    return (t[v & 0xffu] ^ t[256 + ((v >> 8) & 0xffu)]) ^ (t[512 + ((v >> 16) & 0xffu)] ^ t[768 + (v >> 24)]);
+}
+
 template <int TM>
 __device__ __forceinline__ uint32_t absorb4(uint32_t crc, uint4 v, LaneConst L, const uint32_t* tab) {
     if constexpr (TM == TM_S4R) {
@@ -242,21 +311,9 @@ __device__ __forceinline__ uint4 ldg4(const uint4* p) {
 }
 __device__ __forceinline__ uint4 ldg4_plain(const uint4* p) { return *p; }
 
-// How a lane's 512-byte chunk reaches registers.
-enum LoadMode : int {
-    LM_DIRECT_NT = 0,     // lane loads its own chunk, nontemporal (64 lines per instruction)
-    LM_DIRECT = 1,        // same, default cache policy
-    LM_STAGED = 2,        // line-coalesced loads (8 whole lines per instruction) + LDS transpose
-};
-
-// Staging layout (one 8 KiB buffer per wave per round): piece t (16 B) of
-// owner lane i sits in slot t*64 + (i ^ t).  ds_write_b128 by the loading
-// lanes and ds_read_b128 by the owners are both bank-conflict-free.
-__device__ __forceinline__ uint32_t stage_slot(uint32_t owner, uint32_t t) { return t * 64u + (owner ^ t); }
-
-// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
-// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
-// Returns lane 0's first 16 bytes through *hdr.
+// Lane 0 keeps a copy of the block's first 16 bytes (*hdr) and zeroes header
+// bytes 0..5 (force_type: the type byte becomes FULL), so the chunk set covers
+// exactly block[6:32768).
 __device__ __forceinline__ void zero_header_bytes(uint4& v, bool l0, bool force_type, uint4* hdr) {
     *hdr = v;
     v.x = l0 ? 0u : v.x;
@@ -268,54 +325,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Raw register of lane's 512-byte chunk of a full block (header bytes 0..5
-// zeroed for lane 0, so the chunk set covers exactly block[6:32768)).
-// Returns lane 0's first 16 bytes through *hdr.
-template <int TM, int LM>
-__device__ __forceinline__ uint32_t full_block_lane_crc(const uint8_t* blk, LaneConst L, const uint32_t* tab,
-                                                        uint4* stage, uint4* hdr, bool force_type) {
-    const uint32_t lane = lane_id();
-    const bool l0 = lane == 0;
-    uint32_t crc = 0;
-    uint4 cur[8], nxt[8];
-    // Round r covers bytes [512 i + 128 r, +128) of every lane i.
-    auto load_round = [&](uint4* v, int r) {
-        if constexpr (LM == LM_STAGED) {
-            // instruction k: lanes 8m..8m+7 read the whole 128-B line of owner 8k+m
-            const uint8_t* base = blk + (lane >> 3) * 512u + r * 128 + (lane & 7u) * 16u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = ldg4(reinterpret_cast<const uint4*>(base + k * 8 * 512));
-        } else {
-            const uint4* p = reinterpret_cast<const uint4*>(blk + lane * 512u + r * 128);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = LM == LM_DIRECT_NT ? ldg4(p + j) : ldg4_plain(p + j);
-        }
-    };
-    load_round(cur, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        if (r < 3) load_round(nxt, r + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (LM == LM_STAGED) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) stage[stage_slot(8u * k + (lane >> 3), lane & 7u)] = cur[k];
-            wave_lds_sync();
-#pragma unroll
-            for (int t = 0; t < 8; ++t) cur[t] = stage[stage_slot(lane, t)];
-            wave_lds_sync();
-        }
-        if (r == 0) zero_header_bytes(cur[0], l0, force_type, hdr);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) crc = absorb4<TM>(crc, cur[j], L, tab);
-        __builtin_amdgcn_sched_barrier(0);
-        if (r < 3) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
-        }
-    }
-    return crc;
 }
 
 // ---------------------------------------------------------------------------

@@ -24,10 +24,9 @@ struct DeviceInfo {
     int num_cu = 256;
 };
 
-// variant: 0 = production (k_full_blocks4: interleaved word streams, load ring); others are the
-// experiment arms listed in k_blocks.hip (100 = streaming-read ceiling).
-hipError_t crc_full_blocks_variant(const DeviceInfo& di, int variant, const void* d_blocks, uint64_t n,
-                                   uint32_t* d_masked, uint8_t* d_ok, hipStream_t st);
+// k_full_blocks4: interleaved word streams, load ring (k_blocks.hip).
+hipError_t crc_full_blocks(const DeviceInfo& di, const void* d_blocks, uint64_t n, uint32_t* d_masked, uint8_t* d_ok,
+                           hipStream_t st);
 hipError_t frame_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, hipStream_t st);
 hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, uint64_t seed, uint64_t first,
                              hipStream_t st);
@@ -43,6 +42,9 @@ constexpr uint32_t kListCap = 256;
 constexpr uint32_t kListStride = kListCap + 1;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st);
+// u64 words of a header-list buffer for nblocks: the lists, then the verify
+// kernel's list of qualifying blocks (a count and nblocks u32).
+uint64_t hlist_words(uint64_t nblocks);
 // d_tile_scratch: scan_scratch_words(n) u32 of device scratch.
 hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
                               uint32_t* d_tile_scratch, hipStream_t st);
@@ -79,11 +81,12 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
 // at in-block offset lead) the number of records and the fragment index of
 // its first record, and one u64 header-list entry per fragment (written by
 // the scatter); with them the CRC pass reads its header lists instead of
-// walking the headers of every block.
+// walking the headers of every block.  d_blist: nblocks + 1 u32 of scratch for
+// the CRC pass's block list.
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
                          void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st,
                          const uint32_t* d_counts = nullptr, const uint32_t* d_first = nullptr,
-                         uint64_t* d_xlist = nullptr);
+                         uint64_t* d_xlist = nullptr, uint32_t* d_blist = nullptr);
 
 hipError_t batch_count(const DeviceInfo& di, const void* d_payload, uint64_t payload_bytes,
                        const revel_logical_record* d_logical, uint64_t n, revel_batch_info* d_info, uint64_t* d_nent,

@@ -416,6 +416,7 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
     revel::FragDesc* d_frags = nullptr;
     uint32_t *d_counts = nullptr, *d_first = nullptr;
     uint64_t* d_xlist = nullptr;
+    uint32_t* d_blist = nullptr;
     hipError_t e = hipSuccess;
     if (!frags.empty()) {
         e = scratch.get(&d_frags, frags.size());
@@ -426,12 +427,13 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
         if (e == hipSuccess) e = scratch.get(&d_counts, vblocks);
         if (e == hipSuccess) e = scratch.get(&d_first, vblocks);
         if (e == hipSuccess) e = scratch.get(&d_xlist, frags.size());
+        if (e == hipSuccess) e = scratch.get(&d_blist, vblocks + 1);
         if (e == hipSuccess) e = hipMemcpyAsync(d_counts, counts.data(), vblocks * 4, hipMemcpyHostToDevice, st);
         if (e == hipSuccess) e = hipMemcpyAsync(d_first, first.data(), vblocks * 4, hipMemcpyHostToDevice, st);
     }
     if (e == hipSuccess)
         e = revel::frame_records(ctx->di, d_payloads, d_frags, frags.size(), d_image, len, lead, st, d_counts, d_first,
-                                 d_xlist);
+                                 d_xlist, d_blist);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         (void)hipStreamSynchronize(st);  // the context's scratch is free before the next call

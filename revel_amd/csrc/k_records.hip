@@ -321,11 +321,44 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t* __restrict__ hlist, 
 __device__ uint32_t g_x8n_tab[kBlockSize + 1];
 __device__ uint32_t g_init_xor_tab[kBlockSize + 1];
 
+// x^(-8d) for d = 0..32768 (filled with the x^(8d) / init_xor tables).
+__device__ uint32_t g_x8inv_tab[kBlockSize + 1];
+
+struct InvShiftTables {
+    uint32_t chunk[65];  // x^(-8*512*m)
+    uint32_t byte[513];  // x^(-8*d)
+};
+constexpr InvShiftTables make_inv_shift_tables() {
+    InvShiftTables s{};
+    const uint32_t xinv8 = pow_modp(kXInv, 8);
+    const uint32_t xinv4096 = pow_modp(xinv8, 512);
+    uint32_t v = 0x80000000u;
+    for (int m = 0; m <= 64; ++m) {
+        s.chunk[m] = v;
+        v = multmodp(v, xinv4096);
+    }
+    v = 0x80000000u;
+    for (int d = 0; d <= 512; ++d) {
+        s.byte[d] = v;
+        v = multmodp(v, xinv8);
+    }
+    return s;
+}
+__constant__ InvShiftTables c_inv_shift = make_inv_shift_tables();
+static_assert(multmodp(make_inv_shift_tables().byte[7], x8n(7)) == 0x80000000u, "x^-56 * x^56 == 1");
+
+__device__ __forceinline__ uint32_t gf_x8inv_block(uint32_t n) {
+    const uint32_t m = n >> 9, d = n & 511u;
+    const uint32_t a = c_inv_shift.chunk[m];
+    return d ? gf_mul(a, c_inv_shift.byte[d]) : a;
+}
+
 __global__ void k_init_len_tables() {
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d <= kBlockSize; d += gridDim.x * blockDim.x) {
         const uint32_t x = gf_x8n_block(d);
         g_x8n_tab[d] = x;
         g_init_xor_tab[d] = gf_mul(x, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        g_x8inv_tab[d] = gf_x8inv_block(d);
     }
 }
 
@@ -1204,6 +1237,8 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3r(const uint
 
 #include "verify5.inc"
 #include "verify_dense.inc"
+#include "verify_rows.inc"
+constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
 
 // ---------------------------------------------------------------------------
 // Device append framing, step 1: scatter fragments (payload bytes + length
@@ -1356,6 +1391,8 @@ hipError_t exclusive_scan_u64(const DeviceInfo&, const uint64_t* d_in, uint64_t*
 
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
+uint64_t hlist_words(uint64_t nblocks) { return nblocks * kListStride + (nblocks + 2) / 2 + 1; }
+
 // One-time per device (per thread): the x^(8d) / init_xor(d) tables.
 static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
     static thread_local int inited_dev = -1;
@@ -1398,18 +1435,31 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
 // sparse partial blocks through the single-wave verify2 launch.  Each kernel
 // skips the others' blocks by count.  Lists: verify = hlist + overflow entries
 // in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
-template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false, int RING = 0, bool TQ8 = false>
+template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false, int RING = 0, bool TQ8 = false,
+          bool ROWS = false>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
-                                      hipStream_t st) {
+                                      hipStream_t st, uint32_t* d_blist = nullptr) {
     const uint64_t vbytes = nbytes + lead;
     const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize, nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
     auto grid_for = [&](uint64_t n, uint64_t waves) {
         return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + waves - 1) / waves));
     };
     if (b_hi > b_lo) {
-        if constexpr (SPARSE_V5) {
+        if constexpr (ROWS) {
+            // qualifying blocks listed first (d_blist[0] = count, then the list)
+            hipError_t e = hipMemsetAsync(d_blist, 0, 4, st);
+            if (e != hipSuccess) return e;
+            const uint64_t nb = b_hi - b_lo;
+            hipLaunchKernelGGL(k_sparse_blocks,
+                               dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 4, (nb + 255) / 256))),
+                               dim3(256), 0, st, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist + 1, d_blist);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_verify_rows<FRAME, kRowsRing>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
+                               img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + 1, d_blist);
+        } else if constexpr (SPARSE_V5) {
             static_assert(!FRAME, "v5 verifies only");
             hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(b_hi, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
                                nbytes, base_offset, d_first, d_out, hl, d_counts);
@@ -1450,6 +1500,11 @@ static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img, nbytes,
                        base_offset, d_first, d_out, lead, hl, d_counts, reinterpret_cast<const uint64_t*>(d_out), 3u);
     return hipGetLastError();
+}
+
+// The qualifying-block list of verify lives after the header lists (hlist_words).
+static uint32_t* block_list(const uint64_t* hl, uint64_t nblocks) {
+    return reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(hl) + nblocks * kListStride);
 }
 
 hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
@@ -1526,11 +1581,17 @@ hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void*
             return launch_verify_split<false, false, false, false, 2>(di, img, nbytes, base_offset, d_first, d_out,
                                                                       0u, hl, d_counts, xl, xs, st);
         }
+        case 15:  // session-5 production: v3 over the sparse whole blocks
+            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
+            return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                                              reinterpret_cast<const uint64_t*>(d_out),
+                                              (uint32_t)(sizeof(revel_record_result) / 8), st);
         case 0:
             if (hl && d_counts && aligned16(img))
-                return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                                                  reinterpret_cast<const uint64_t*>(d_out),
-                                                  (uint32_t)(sizeof(revel_record_result) / 8), st);
+                return launch_verify_split<false, false, false, false, 0, false, true>(
+                    di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                    reinterpret_cast<const uint64_t*>(d_out), (uint32_t)(sizeof(revel_record_result) / 8), st,
+                    block_list(hl, nblocks));
             [[fallthrough]];
         case 8:  // session-2 production: v3 over every whole block
         case 2: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
@@ -1562,7 +1623,7 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
 
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
                          void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st, const uint32_t* d_counts,
-                         const uint32_t* d_first, uint64_t* d_xlist) {
+                         const uint32_t* d_first, uint64_t* d_xlist, uint32_t* d_blist) {
     if (nfrags) {
         const bool small = image_len / nfrags <= 1024u;
         const uint64_t per_wg = small ? 96 : 32;  // 4 waves x 8 groups x FPG
@@ -1587,9 +1648,10 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     const bool partial = lead != 0 || (image_len + lead) % kBlockSize != 0;
     const bool lists = d_counts && d_first && d_xlist;
-    if (lists && aligned16(d_image))
-        return launch_verify_split<true>(di, static_cast<const uint8_t*>(d_image), image_len, 0ull, d_first, nullptr,
-                                         lead, nullptr, d_counts, d_xlist, 1u, st);
+    if (lists && aligned16(d_image) && d_blist)
+        return launch_verify_split<true, false, false, false, 0, false, true>(
+            di, static_cast<const uint8_t*>(d_image), image_len, 0ull, d_first, nullptr, lead, nullptr, d_counts,
+            d_xlist, 1u, st, d_blist);
     return launch_verify3<true>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull,
                                 lists ? d_first : nullptr, nullptr, lead, nullptr, lists ? d_counts : nullptr, st,
                                 lists ? d_xlist : nullptr, 1u);

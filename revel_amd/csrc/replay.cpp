@@ -93,7 +93,7 @@ int ring_init(Ring& R, int nbuf) {
         if (R.mode == REVEL_REPLAY_RECORDS) {
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_counts), nblocks * 4), "hipMalloc(counts)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_first), nblocks * 4), "hipMalloc(first)");
-            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), nblocks * revel::kListStride * 8), "hipMalloc(hlist)");
+            TRY(hipMalloc(reinterpret_cast<void**>(&x.d_hlist), revel::hlist_words(nblocks) * 8), "hipMalloc(hlist)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_scan), revel::scan_scratch_words(nblocks) * 4), "hipMalloc(scan)");
             TRY(hipMalloc(reinterpret_cast<void**>(&x.d_res), nblocks * kMaxRecordsPerBlock * sizeof(revel_record_result)),
                 "hipMalloc(records)");
@@ -261,7 +261,7 @@ int replay(revel_gpu_context* ctx, uint64_t length, uint64_t base_offset, int mo
             TRY(revel::summarize_records(ctx->di, x.d_res, x.d_first, x.d_counts, nblocks, x.d_sum, comp),
                 "summarize_records");
         } else {
-            TRY(revel::crc_full_blocks_variant(ctx->di, 0, x.d, nblocks, x.d_masked, x.d_ok, comp), "crc_full_blocks");
+            TRY(revel::crc_full_blocks(ctx->di, x.d, nblocks, x.d_masked, x.d_ok, comp), "crc_full_blocks");
             TRY(revel::summarize_blocks(ctx->di, x.d_ok, nblocks, base_offset + off, x.d_sum, comp),
                 "summarize_blocks");
         }

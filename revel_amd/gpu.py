@@ -149,11 +149,12 @@ class GpuContext:
         if ok_out is not None and ok_out.nbytes < nblocks:
             raise ValueError("ok buffer too small")
         ok = ok_out.ptr if ok_out is not None else None
-        if variant is None:
+        if variant is None or variant == 0:
             check(lib().revel_gpu_crc_full_blocks(self._h, blocks.ptr, nblocks, masked_out.ptr, ok, None))
         else:
-            check(lib().revel_gpu_crc_full_blocks_variant(self._h, variant, blocks.ptr, nblocks,
-                                                          masked_out.ptr, ok, None))
+            from ._lib import experiments  # kernel variants kept for the record (tools/experiments)
+            check(experiments().revel_x_crc_full_blocks_variant(self._h, variant, blocks.ptr, nblocks,
+                                                                masked_out.ptr, ok, None))
 
     def frame_full_blocks(self, blocks: DeviceBuffer, nblocks: int) -> None:
         if blocks.nbytes < nblocks * BLOCK_SIZE:
