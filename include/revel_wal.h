@@ -78,6 +78,38 @@ int revel_writable_file_sync(revel_writable_file* f);
 int revel_memory_writable_file_contents(const revel_writable_file* f, const uint8_t** data, size_t* n);
 void revel_writable_file_free(revel_writable_file* f);
 
+/* Caller-implemented files: the adapter for a `dyn WritableFile` the caller
+ * owns and shares (Writer::new(Rc<RefCell<dyn WritableFile>>),
+ * log_writer.rs:26,41-45; db.rs:56-63 keeps a clone to sync it) -- every
+ * call of the trait (env.rs:40-50) goes to the matching callback with `user`.
+ * Callbacks return 0 for Ok or an error.rs code (1..5; anything else is
+ * reported as REVEL_IO_ERROR), which the calling entry point returns.
+ * append is required; flush/close/sync may be NULL (no-op, Ok).  release
+ * (nullable) is called once by revel_writable_file_free, e.g. to drop the
+ * Rc clone behind `user`.  On failure nothing is called and the caller keeps
+ * `user`. */
+typedef int (*revel_file_append_fn)(void* user, const uint8_t* data, size_t n);
+typedef int (*revel_file_op_fn)(void* user);
+typedef void (*revel_file_release_fn)(void* user);
+int revel_writable_file_from_callbacks(void* user, revel_file_append_fn append, revel_file_op_fn flush,
+                                       revel_file_op_fn close, revel_file_op_fn sync,
+                                       revel_file_release_fn release, revel_writable_file** out);
+
+/* The adapter for a caller's `Box<dyn SequentialFile>` (env.rs:52-57) handed
+ * to Reader::new (log_reader.rs:40,62).  read fills up to n bytes of scratch
+ * and stores the count in *got (0 = end of file); short counts are allowed,
+ * the library calls again until n bytes or end of file (as it does for
+ * read(2)).  skip(n) advances the position by n bytes (relative; the Posix
+ * reference seeks absolute, env.rs:171-174, which is the same at the only
+ * call, a reader's start); NULL = read and drop.  release (nullable) is called
+ * once when the file is freed -- by revel_sequential_file_free or by the
+ * reader that owns it -- e.g. to drop the Box behind `user`.  On failure
+ * nothing is called and the caller keeps `user`. */
+typedef int (*revel_file_read_fn)(void* user, uint8_t* scratch, size_t n, size_t* got);
+typedef int (*revel_file_skip_fn)(void* user, uint64_t n);
+int revel_sequential_file_from_callbacks(void* user, revel_file_read_fn read, revel_file_skip_fn skip,
+                                         revel_file_release_fn release, revel_sequential_file** out);
+
 /* env.rs:232-246 `MemorySequentialFile::new(Rc<Vec<u8>>)` -- copies data. */
 revel_sequential_file* revel_memory_sequential_file_new(const uint8_t* data, size_t n);
 /* Posix sequential file.  The reference declares PosixSequentialFile
@@ -109,21 +141,36 @@ void revel_log_writer_free(revel_log_writer* w);
 typedef struct revel_gpu_context revel_gpu_context;
 /* Number of visible gfx950 devices (0 on a host without one). */
 int revel_gpu_device_count(int* count);
-/* One context per (thread, device): owns a HIP stream and scratch. */
+/* One context per (thread, device): owns a HIP stream and scratch.  Every
+ * GPU entry point binds the context's device for the duration of the call and
+ * restores the calling thread's current device before it returns. */
 int revel_gpu_context_new(int device, revel_gpu_context** out);
+/* Readers created on a context pin it: freeing a context while readers
+ * still use it is allowed and defers the release to the last reader's
+ * revel_log_reader_free (the context must not be used for anything else
+ * after this call). */
 void revel_gpu_context_free(revel_gpu_context* ctx);
+/* Drop the window buffers a freed reader parked on the context for the next
+ * reader (pinned + device memory of about twice its window). */
+int revel_gpu_context_trim(revel_gpu_context* ctx);
 /* The context's stream as an opaque hipStream_t. */
 void* revel_gpu_context_stream(revel_gpu_context* ctx);
 
 /* ---- log reader: src/log_reader.rs ------------------------------------- */
 typedef struct revel_log_reader revel_log_reader;
-/* log_reader.rs:62-74 `Reader::new(file, checksum, initial_offset)`.
+/* log_reader.rs:62-74 `Reader::new(file, checksum, initial_offset)`:
+ * revel_log_reader_new(file, checksum, initial_offset, NULL, 0, &r) is the
+ * reference's 3-argument constructor.
  * The reader takes ownership of `file` (Box<dyn SequentialFile>) in every
  * case: on failure the file has been freed.
- * With checksum != 0 every physical record's CRC is verified ON THE GPU of
- * `gpu` (required: REVEL_NOT_SUPPORT if NULL); with checksum == 0, gpu may
- * be NULL.  `window_bytes` = bytes read + verified per GPU batch (rounded
- * up to a block multiple; 0 = default 64 MiB). */
+ * With checksum != 0 every physical record's CRC is verified ON THE GPU:
+ * that of `gpu`, or with gpu == NULL of the calling thread's default context
+ * (one per thread and current HIP device, created on first use, released when
+ * the thread exits; REVEL_NOT_SUPPORT when the current device is not gfx950
+ * -- there is no CPU fallback).  With checksum == 0 no GPU is used when gpu
+ * is NULL.  The reader pins its context (see revel_gpu_context_free).
+ * `window_bytes` = bytes read + verified per GPU batch (rounded up to a
+ * block multiple; 0 = default 64 MiB). */
 int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t initial_offset,
                          revel_gpu_context* gpu, size_t window_bytes, revel_log_reader** out);
 /* log_reader.rs:76-153 `read_record(&mut self, scratch) -> Result<Slice>`.

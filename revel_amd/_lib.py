@@ -57,6 +57,13 @@ BATCH_HEADER = 12
 TYPE_DELETION, TYPE_VALUE = 0, 1
 BATCH_OK, BATCH_TOO_SMALL, BATCH_BAD_ENTRY, BATCH_BAD_TAG, BATCH_WRONG_COUNT, BATCH_NOT_RECORD = 0, 1, 2, 3, 4, 5
 
+# callback types of the caller-implemented files (revel_wal.h)
+APPEND_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t)
+FILE_OP_FN = ctypes.CFUNCTYPE(c_int, c_void_p)
+RELEASE_FN = ctypes.CFUNCTYPE(None, c_void_p)
+READ_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, POINTER(c_size_t))
+SKIP_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_uint64)
+
 # name -> (restype, argtypes); every symbol declared in include/revel_wal.h
 SIGNATURES = {
     "revel_crc32c_value": (c_uint32, [c_void_p, c_size_t]),
@@ -71,6 +78,9 @@ SIGNATURES = {
     "revel_writable_file_sync": (c_int, [c_void_p]),
     "revel_memory_writable_file_contents": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
     "revel_writable_file_free": (None, [c_void_p]),
+    "revel_writable_file_from_callbacks": (c_int, [c_void_p, APPEND_FN, FILE_OP_FN, FILE_OP_FN, FILE_OP_FN,
+                                                   RELEASE_FN, POINTER(c_void_p)]),
+    "revel_sequential_file_from_callbacks": (c_int, [c_void_p, READ_FN, SKIP_FN, RELEASE_FN, POINTER(c_void_p)]),
     "revel_memory_sequential_file_new": (c_void_p, [c_void_p, c_size_t]),
     "revel_posix_sequential_file_new": (c_int, [c_char_p, POINTER(c_void_p)]),
     "revel_sequential_file_read": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_size_t)]),
@@ -84,6 +94,7 @@ SIGNATURES = {
     "revel_gpu_context_new": (c_int, [c_int, POINTER(c_void_p)]),
     "revel_gpu_context_free": (None, [c_void_p]),
     "revel_gpu_context_stream": (c_void_p, [c_void_p]),
+    "revel_gpu_context_trim": (c_int, [c_void_p]),
     "revel_log_reader_new": (c_int, [c_void_p, c_int, c_uint64, c_void_p, c_size_t, POINTER(c_void_p)]),
     "revel_log_reader_read_record": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
     "revel_log_reader_last_record_offset": (c_uint64, [c_void_p]),
@@ -121,10 +132,10 @@ SIGNATURES = {
                                         POINTER(ReplayStats)]),
 }
 
-# exported experiment hooks (not part of the public header)
+# exported test hook (not part of the public header): production verify paths
 EXTRA_SIGNATURES = {
-    "revel_gpu_verify_records_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
-                                                 c_void_p, c_void_p]),
+    "revel_gpu_verify_records_path": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
+                                              c_void_p, c_void_p]),
 }
 
 # tools/experiments/libexperiments.so: kernel variants kept for the record
@@ -133,6 +144,8 @@ EXPERIMENT_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(_
 EXPERIMENT_SIGNATURES = {
     "revel_x_crc_full_blocks_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p,
                                                 c_void_p]),
+    "revel_x_verify_records_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
+                                               c_void_p, c_void_p]),
 }
 _xlib = None
 

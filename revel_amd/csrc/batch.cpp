@@ -17,7 +17,8 @@ extern "C" int revel_gpu_decode_batches(revel_gpu_context* ctx, const void* d_pa
     if (nlogical == 0) return REVEL_OK;
     if (!d_payload || !d_logical || !d_info || (entries_cap && !d_entries))
         return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const uint64_t n = nlogical;
     revel::DeviceScratch S(&ctx->arena);

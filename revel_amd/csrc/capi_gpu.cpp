@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "gpu_internal.h"
 
@@ -30,6 +31,73 @@ int set_error(int code, const char* fmt, ...) {
 
 using revel::set_error;
 
+namespace revel {
+
+void destroy_context(revel_gpu_context* ctx) {
+    DeviceGuard guard(ctx->di.device);
+    if (ctx->stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    if (ctx->hlist) (void)hipFree(ctx->hlist);
+    if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
+    if (ctx->arena.base) (void)hipFree(ctx->arena.base);
+    auto& pr = ctx->parked_reader;
+    if (pr.h_win) (void)hipHostFree(pr.h_win);
+    if (pr.d_win) (void)hipFree(pr.d_win);
+    if (pr.d_counts) (void)hipFree(pr.d_counts);
+    if (pr.d_first) (void)hipFree(pr.d_first);
+    if (pr.d_out) (void)hipFree(pr.d_out);
+    delete ctx;
+}
+
+void context_pin(revel_gpu_context* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->life_mu);
+    ++ctx->readers;
+}
+
+void context_unpin(revel_gpu_context* ctx) {
+    bool destroy;
+    {
+        std::lock_guard<std::mutex> lk(ctx->life_mu);
+        destroy = --ctx->readers == 0 && ctx->free_requested;
+    }
+    if (destroy) destroy_context(ctx);
+}
+
+namespace {
+// One default context per (thread, device), released when the thread exits
+// (deferred to the last reader, like any context).
+struct ThreadDefaults {
+    std::vector<revel_gpu_context*> by_device;
+    ~ThreadDefaults() {
+        for (revel_gpu_context* c : by_device)
+            if (c) revel_gpu_context_free(c);
+    }
+};
+thread_local ThreadDefaults t_defaults;
+}  // namespace
+
+int default_context(revel_gpu_context** out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_error(REVEL_NOT_SUPPORT, "no HIP device visible: checksum verification needs a gfx950 GPU");
+    }
+    auto& v = t_defaults.by_device;
+    if ((size_t)dev < v.size() && v[dev]) {
+        *out = v[dev];
+        return REVEL_OK;
+    }
+    int rc = revel_gpu_context_new(dev, out);
+    if (rc) return rc;
+    if (v.size() <= (size_t)dev) v.resize(dev + 1, nullptr);
+    v[dev] = *out;
+    return REVEL_OK;
+}
+
+}  // namespace revel
+
 namespace {
 
 int hip_fail(hipError_t e, const char* what) {
@@ -42,21 +110,16 @@ bool is_gfx950(int dev) {
     return strncmp(p.gcnArchName, "gfx950", 6) == 0;
 }
 
-struct Bind {
-    hipError_t err;
-    explicit Bind(const revel_gpu_context* c) : err(hipSetDevice(c->di.device)) {}
-};
-
 hipStream_t pick(const revel_gpu_context* c, void* stream) {
     return stream ? static_cast<hipStream_t>(stream) : c->stream;
 }
 
-#define CHECK_CTX(ctx)                                                                        \
-    do {                                                                                      \
-        if (!(ctx)) return set_error(REVEL_INVALID_ARGUMENT, "null revel_gpu_context");     \
-        Bind bind_(ctx);                                                                      \
-        if (bind_.err != hipSuccess) return hip_fail(bind_.err, "hipSetDevice");             \
-    } while (0)
+// Validates the context and binds its device for the rest of the calling
+// function (restoring the caller's device on return).
+#define CHECK_CTX(ctx)                                                                     \
+    if (!(ctx)) return set_error(REVEL_INVALID_ARGUMENT, "null revel_gpu_context");        \
+    revel::DeviceGuard device_guard_((ctx)->di.device);                                     \
+    if (device_guard_.err() != hipSuccess) return hip_fail(device_guard_.err(), "hipSetDevice")
 
 #define HIP_TRY(expr, what)                          \
     do {                                             \
@@ -94,7 +157,8 @@ int revel_gpu_context_new(int device, revel_gpu_context** out) {
     }
     if (device < 0 || device >= n) return set_error(REVEL_INVALID_ARGUMENT, "device %d out of range (0..%d)", device, n - 1);
     if (!is_gfx950(device)) return set_error(REVEL_NOT_SUPPORT, "device %d is not gfx950", device);
-    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    revel::DeviceGuard guard(device);
+    if (guard.err() != hipSuccess) return hip_fail(guard.err(), "hipSetDevice");
     auto* c = new revel_gpu_context;
     c->di.device = device;
     int cu = 0;
@@ -110,21 +174,26 @@ int revel_gpu_context_new(int device, revel_gpu_context** out) {
 
 void revel_gpu_context_free(revel_gpu_context* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->di.device);
-    if (ctx->stream) {
-        (void)hipStreamSynchronize(ctx->stream);
-        (void)hipStreamDestroy(ctx->stream);
+    {
+        std::lock_guard<std::mutex> lk(ctx->life_mu);
+        if (ctx->readers > 0) {  // the last reader's release destroys it
+            ctx->free_requested = true;
+            return;
+        }
     }
-    if (ctx->hlist) (void)hipFree(ctx->hlist);
-    if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
-    if (ctx->arena.base) (void)hipFree(ctx->arena.base);
+    revel::destroy_context(ctx);
+}
+
+int revel_gpu_context_trim(revel_gpu_context* ctx) {
+    CHECK_CTX(ctx);
     auto& pr = ctx->parked_reader;
-    if (pr.h_win) (void)hipHostFree(pr.h_win);
-    if (pr.d_win) (void)hipFree(pr.d_win);
-    if (pr.d_counts) (void)hipFree(pr.d_counts);
-    if (pr.d_first) (void)hipFree(pr.d_first);
-    if (pr.d_out) (void)hipFree(pr.d_out);
-    delete ctx;
+    if (pr.h_win) HIP_TRY(hipHostFree(pr.h_win), "hipHostFree");
+    if (pr.d_win) HIP_TRY(hipFree(pr.d_win), "hipFree");
+    if (pr.d_counts) HIP_TRY(hipFree(pr.d_counts), "hipFree");
+    if (pr.d_first) HIP_TRY(hipFree(pr.d_first), "hipFree");
+    if (pr.d_out) HIP_TRY(hipFree(pr.d_out), "hipFree");
+    pr = revel_gpu_context::ParkedReader{};
+    return REVEL_OK;
 }
 
 void* revel_gpu_context_stream(revel_gpu_context* ctx) { return ctx ? ctx->stream : nullptr; }
@@ -208,18 +277,21 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     return REVEL_OK;
 }
 
-// Experiment hook (not in the public header): 0 = production, 1 = round-1 kernel.
-int revel_gpu_verify_records_variant(revel_gpu_context* ctx, int variant, const void* d_image, size_t nbytes,
-                                     uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                     void* stream) {
+// Test hook (not in the public header): the production verify paths of
+// revel::verify_records_path (0 = production, 1 = header walk without the
+// count pass's lists, 2 = v3 with the lists).
+int revel_gpu_verify_records_path(revel_gpu_context* ctx, int path, const void* d_image, size_t nbytes,
+                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                  void* stream) {
     CHECK_CTX(ctx);
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    if (path < 0 || path > 2) return set_error(REVEL_INVALID_ARGUMENT, "verify path %d", path);
     const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
-    HIP_TRY(revel::verify_records_variant(ctx->di, variant, d_image, nbytes, base_offset, d_first, d_out,
-                                          memo ? ctx->hlist : nullptr, memo ? ctx->hlist_counts : nullptr,
-                                          pick(ctx, stream)),
-            "verify_records_variant launch");
+    HIP_TRY(revel::verify_records_path(ctx->di, path, d_image, nbytes, base_offset, d_first, d_out,
+                                       memo ? ctx->hlist : nullptr, memo ? ctx->hlist_counts : nullptr,
+                                       pick(ctx, stream)),
+            "verify_records_path launch");
     ctx->hlist_image = nullptr;
     return REVEL_OK;
 }

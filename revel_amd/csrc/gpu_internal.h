@@ -5,7 +5,11 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "revel_wal.h"
+
+struct revel_gpu_context;
 
 namespace revel {
 
@@ -59,15 +63,12 @@ hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, u
 hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
                         const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
                         hipStream_t st);
-// C3 verify variants: 0 = production (k_verify_records3 whole blocks + a
-// single-wave launch for partial blocks; header list when given), 1 = round-1
-// kernel (v1), 2 = production forced to walk headers itself, 3 / 4 = v2 with
-// the masked boundary path (with / without the wave vote), 5 = v2 as one
-// kernel for whole and partial blocks, 6 = v2 split into whole/partial launches.
-// Other values: hipErrorInvalidValue.
-hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
-                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                  const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st);
+// C3 verify paths (test hook): 0 = production, 1 = v3 walking the headers
+// itself, 2 = v3 with the count pass's header lists.  Other values:
+// hipErrorInvalidValue.  The experiment arms are in tools/experiments.
+hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_image, uint64_t nbytes,
+                               uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                               const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st);
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                           const uint32_t* d_counts, hipStream_t st);
@@ -148,6 +149,44 @@ struct DeviceScratch {
 // Set the thread-local error string; returns code.
 int set_error(int code, const char* fmt, ...);
 
+// Binds `device` on the calling thread for the lifetime of the guard and
+// restores the thread's previous current device afterwards, so a C-ABI call
+// never moves the caller's later HIP (or torch) work to another GPU.
+class DeviceGuard {
+   public:
+    explicit DeviceGuard(int device) : want_(device) {
+        if (hipGetDevice(&prev_) != hipSuccess) {
+            (void)hipGetLastError();
+            prev_ = -1;
+        }
+        err_ = prev_ == device ? hipSuccess : hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        if (err_ == hipSuccess && prev_ >= 0 && prev_ != want_) (void)hipSetDevice(prev_);
+    }
+    hipError_t err() const { return err_; }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+   private:
+    int want_;
+    int prev_ = -1;
+    hipError_t err_ = hipSuccess;
+};
+
+// Releases the context's resources now (no readers left).  Internal: the
+// public revel_gpu_context_free defers to the last reader.
+void destroy_context(revel_gpu_context* ctx);
+// Reader lifetime bookkeeping: a reader pins its context; the context is
+// destroyed by whichever comes last, revel_gpu_context_free or the release
+// of its last reader.
+void context_pin(revel_gpu_context* ctx);
+void context_unpin(revel_gpu_context* ctx);
+// The calling thread's default context on its current HIP device (created on
+// first use, owned by the thread; released at thread exit).  NOT_SUPPORT when
+// the current device is not gfx950.
+int default_context(revel_gpu_context** out);
+
 }  // namespace revel
 
 struct revel_gpu_context {
@@ -176,4 +215,10 @@ struct revel_gpu_context {
         revel_record_result* d_out = nullptr;
         size_t d_out_cap = 0;
     } parked_reader;
+    // Lifetime: live readers pin the context; revel_gpu_context_free with
+    // readers still alive only marks it, and the last reader's release
+    // destroys it (revel_wal.h, "GPU context").
+    std::mutex life_mu;
+    int readers = 0;
+    bool free_requested = false;
 };

@@ -74,19 +74,29 @@ uint32_t revel_crc32c_unmask(uint32_t masked) { return revel::unmask(masked); }
 // Files (env.rs)
 // ===========================================================================
 struct revel_writable_file {
-    bool memory = true;
+    enum Kind { MEMORY, POSIX, CALLBACK } kind = MEMORY;
     std::vector<uint8_t> mem;
     int fd = -1;
     std::vector<uint8_t> buf;  // posix write buffer, env.rs:69 kWritableFileBufferSize
     size_t pos = 0;
     std::string path;
+    // CALLBACK: the caller's `dyn WritableFile` (env.rs:40-50)
+    void* user = nullptr;
+    revel_file_append_fn cb_append = nullptr;
+    revel_file_op_fn cb_flush = nullptr, cb_close = nullptr, cb_sync = nullptr;
+    revel_file_release_fn cb_release = nullptr;
 };
 
 struct revel_sequential_file {
-    bool memory = true;
+    enum Kind { MEMORY, POSIX, CALLBACK } kind = MEMORY;
     std::vector<uint8_t> mem;
     size_t off = 0;
     int fd = -1;
+    // CALLBACK: the caller's `dyn SequentialFile` (env.rs:52-57)
+    void* user = nullptr;
+    revel_file_read_fn cb_read = nullptr;
+    revel_file_skip_fn cb_skip = nullptr;
+    revel_file_release_fn cb_release = nullptr;
 };
 
 namespace {
@@ -112,6 +122,18 @@ int posix_flush_buffer(revel_writable_file* f) {
     return rc;
 }
 
+// A caller callback's status: 0 = Ok, 1..5 = the error.rs code it returned,
+// anything else is reported as IOError.
+int callback_status(int rc, const char* what) {
+    if (rc == REVEL_OK) return REVEL_OK;
+    const int code = rc >= REVEL_NOT_FOUND && rc <= REVEL_IO_ERROR ? rc : REVEL_IO_ERROR;
+    return set_error(code, "%s callback returned %d", what, rc);
+}
+
+int callback_op(revel_file_op_fn fn, void* user, const char* what) {
+    return fn ? callback_status(fn(user), what) : REVEL_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -124,7 +146,7 @@ int revel_posix_writable_file_new(const char* path, revel_writable_file** out) {
     int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
     if (fd < 0) return set_error(REVEL_IO_ERROR, "open(%s): %s", path, strerror(errno));
     auto* f = new revel_writable_file;
-    f->memory = false;
+    f->kind = revel_writable_file::POSIX;
     f->fd = fd;
     f->buf.resize(kWritableFileBufferSize);
     f->path = path;
@@ -132,13 +154,32 @@ int revel_posix_writable_file_new(const char* path, revel_writable_file** out) {
     return REVEL_OK;
 }
 
+int revel_writable_file_from_callbacks(void* user, revel_file_append_fn append, revel_file_op_fn flush,
+                                       revel_file_op_fn close, revel_file_op_fn sync, revel_file_release_fn release,
+                                       revel_writable_file** out) {
+    if (!out) return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    if (!append) return set_error(REVEL_INVALID_ARGUMENT, "append callback is required");
+    auto* f = new revel_writable_file;
+    f->kind = revel_writable_file::CALLBACK;
+    f->user = user;
+    f->cb_append = append;
+    f->cb_flush = flush;
+    f->cb_close = close;
+    f->cb_sync = sync;
+    f->cb_release = release;
+    *out = f;
+    return REVEL_OK;
+}
+
 // env.rs:116-136 intent: buffer small appends, write large ones directly.
 int revel_writable_file_append(revel_writable_file* f, const uint8_t* data, size_t n) {
     if (!f || (!data && n)) return set_error(REVEL_INVALID_ARGUMENT, "null file/data");
-    if (f->memory) {
+    if (f->kind == revel_writable_file::MEMORY) {
         f->mem.insert(f->mem.end(), data, data + n);
         return REVEL_OK;
     }
+    if (f->kind == revel_writable_file::CALLBACK) return callback_status(f->cb_append(f->user, data, n), "append");
     if (f->fd < 0) return set_error(REVEL_IO_ERROR, "append to closed file");
     size_t copy = std::min(n, kWritableFileBufferSize - f->pos);
     memcpy(f->buf.data() + f->pos, data, copy);
@@ -158,14 +199,16 @@ int revel_writable_file_append(revel_writable_file* f, const uint8_t* data, size
 
 int revel_writable_file_flush(revel_writable_file* f) {
     if (!f) return set_error(REVEL_INVALID_ARGUMENT, "null file");
-    if (f->memory) return REVEL_OK;
+    if (f->kind == revel_writable_file::MEMORY) return REVEL_OK;
+    if (f->kind == revel_writable_file::CALLBACK) return callback_op(f->cb_flush, f->user, "flush");
     if (f->fd < 0) return set_error(REVEL_IO_ERROR, "flush of closed file");
     return posix_flush_buffer(f);
 }
 
 int revel_writable_file_close(revel_writable_file* f) {
     if (!f) return set_error(REVEL_INVALID_ARGUMENT, "null file");
-    if (f->memory || f->fd < 0) return REVEL_OK;
+    if (f->kind == revel_writable_file::CALLBACK) return callback_op(f->cb_close, f->user, "close");
+    if (f->kind == revel_writable_file::MEMORY || f->fd < 0) return REVEL_OK;
     int rc = posix_flush_buffer(f);
     if (::close(f->fd) != 0 && rc == REVEL_OK) rc = set_error(REVEL_IO_ERROR, "close: %s", strerror(errno));
     f->fd = -1;
@@ -174,7 +217,8 @@ int revel_writable_file_close(revel_writable_file* f) {
 
 int revel_writable_file_sync(revel_writable_file* f) {
     if (!f) return set_error(REVEL_INVALID_ARGUMENT, "null file");
-    if (f->memory) return REVEL_OK;
+    if (f->kind == revel_writable_file::MEMORY) return REVEL_OK;
+    if (f->kind == revel_writable_file::CALLBACK) return callback_op(f->cb_sync, f->user, "sync");
     if (f->fd < 0) return set_error(REVEL_IO_ERROR, "sync of closed file");
     int rc = posix_flush_buffer(f);
     if (rc) return rc;
@@ -184,7 +228,7 @@ int revel_writable_file_sync(revel_writable_file* f) {
 
 int revel_memory_writable_file_contents(const revel_writable_file* f, const uint8_t** data, size_t* n) {
     if (!f || !data || !n) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
-    if (!f->memory) return set_error(REVEL_INVALID_ARGUMENT, "not a memory file");
+    if (f->kind != revel_writable_file::MEMORY) return set_error(REVEL_INVALID_ARGUMENT, "not a memory file");
     *data = f->mem.data();
     *n = f->mem.size();
     return REVEL_OK;
@@ -192,7 +236,8 @@ int revel_memory_writable_file_contents(const revel_writable_file* f, const uint
 
 void revel_writable_file_free(revel_writable_file* f) {
     if (!f) return;
-    if (!f->memory && f->fd >= 0) (void)revel_writable_file_close(f);
+    if (f->kind == revel_writable_file::POSIX && f->fd >= 0) (void)revel_writable_file_close(f);
+    if (f->kind == revel_writable_file::CALLBACK && f->cb_release) f->cb_release(f->user);
     delete f;
 }
 
@@ -209,8 +254,23 @@ int revel_posix_sequential_file_new(const char* path, revel_sequential_file** ou
     if (fd < 0) return set_error(errno == ENOENT ? REVEL_NOT_FOUND : REVEL_IO_ERROR, "open(%s): %s", path,
                                  strerror(errno));
     auto* f = new revel_sequential_file;
-    f->memory = false;
+    f->kind = revel_sequential_file::POSIX;
     f->fd = fd;
+    *out = f;
+    return REVEL_OK;
+}
+
+int revel_sequential_file_from_callbacks(void* user, revel_file_read_fn read, revel_file_skip_fn skip,
+                                         revel_file_release_fn release, revel_sequential_file** out) {
+    if (!out) return set_error(REVEL_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    if (!read) return set_error(REVEL_INVALID_ARGUMENT, "read callback is required");
+    auto* f = new revel_sequential_file;
+    f->kind = revel_sequential_file::CALLBACK;
+    f->user = user;
+    f->cb_read = read;
+    f->cb_skip = skip;
+    f->cb_release = release;
     *out = f;
     return REVEL_OK;
 }
@@ -218,7 +278,7 @@ int revel_posix_sequential_file_new(const char* path, revel_sequential_file** ou
 int revel_sequential_file_read(revel_sequential_file* f, uint8_t* scratch, size_t n, size_t* got) {
     if (!f || !got || (!scratch && n)) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
     *got = 0;
-    if (f->memory) {
+    if (f->kind == revel_sequential_file::MEMORY) {
         size_t avail = f->off < f->mem.size() ? f->mem.size() - f->off : 0;
         size_t k = std::min(n, avail);
         if (k) memcpy(scratch, f->mem.data() + f->off, k);
@@ -226,9 +286,19 @@ int revel_sequential_file_read(revel_sequential_file* f, uint8_t* scratch, size_
         *got = k;
         return REVEL_OK;
     }
-    // fill as much as the file has (read(2) may return short counts)
+    // fill as much as the file has: read(2) and a caller's read may both
+    // return short counts before the end of the file
     size_t total = 0;
     while (total < n) {
+        if (f->kind == revel_sequential_file::CALLBACK) {
+            size_t k = 0;
+            int rc = callback_status(f->cb_read(f->user, scratch + total, n - total, &k), "read");
+            if (rc) return rc;
+            if (k > n - total) return set_error(REVEL_IO_ERROR, "read callback filled %zu of %zu bytes", k, n - total);
+            if (k == 0) break;
+            total += k;
+            continue;
+        }
         ssize_t r = ::read(f->fd, scratch + total, n - total);
         if (r < 0) {
             if (errno == EINTR) continue;
@@ -243,8 +313,20 @@ int revel_sequential_file_read(revel_sequential_file* f, uint8_t* scratch, size_
 
 int revel_sequential_file_skip(revel_sequential_file* f, uint64_t n) {
     if (!f) return set_error(REVEL_INVALID_ARGUMENT, "null file");
-    if (f->memory) {
+    if (f->kind == revel_sequential_file::MEMORY) {
         f->off += n;
+        return REVEL_OK;
+    }
+    if (f->kind == revel_sequential_file::CALLBACK) {
+        if (f->cb_skip) return callback_status(f->cb_skip(f->user, n), "skip");
+        uint8_t sink[4096];  // no skip callback: read and drop
+        while (n) {
+            size_t k = 0;
+            int rc = revel_sequential_file_read(f, sink, (size_t)std::min<uint64_t>(n, sizeof sink), &k);
+            if (rc) return rc;
+            if (k == 0) break;
+            n -= k;
+        }
         return REVEL_OK;
     }
     if (::lseek(f->fd, (off_t)n, SEEK_CUR) < 0) return set_error(REVEL_IO_ERROR, "lseek: %s", strerror(errno));
@@ -253,7 +335,8 @@ int revel_sequential_file_skip(revel_sequential_file* f, uint64_t n) {
 
 void revel_sequential_file_free(revel_sequential_file* f) {
     if (!f) return;
-    if (!f->memory && f->fd >= 0) ::close(f->fd);
+    if (f->kind == revel_sequential_file::POSIX && f->fd >= 0) ::close(f->fd);
+    if (f->kind == revel_sequential_file::CALLBACK && f->cb_release) f->cb_release(f->user);
     delete f;
 }
 
@@ -395,7 +478,8 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
     if (len > image_cap) return set_error(REVEL_INVALID_ARGUMENT, "image capacity %zu < %llu", image_cap,
                                           (unsigned long long)len);
     if (len && (!d_image || (!d_payloads && frags.size()))) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     // Header lists for the device CRC pass: per virtual block (image byte 0 at
     // in-block offset `lead`) its record count and the fragment index of its
@@ -566,10 +650,33 @@ int load_window(revel_log_reader* r) {
     return REVEL_OK;
 }
 
+// Device + pinned bytes a parked reader may keep on its context: the window
+// twice (pinned + device) plus results up to twice the window's bytes.
+bool parkable(const revel_log_reader* r) {
+    return r->d_out_cap * sizeof(revel_record_result) <= 2 * r->window;
+}
+
+void free_parked(revel_gpu_context* g) {
+    auto& pr = g->parked_reader;
+    if (pr.h_win) revel_gpu_host_free(g, pr.h_win);
+    revel_gpu_free(g, pr.d_win);
+    revel_gpu_free(g, pr.d_counts);
+    revel_gpu_free(g, pr.d_first);
+    revel_gpu_free(g, pr.d_out);
+    pr = revel_gpu_context::ParkedReader{};
+}
+
 void reader_release(revel_log_reader* r) {
-    if (r->gpu && r->win && r->d_win && r->d_counts && r->d_first) {
-        auto& pr = r->gpu->parked_reader;
-        if (!pr.h_win) {  // park the window buffers for the next reader on this context
+    revel_gpu_context* g = r->gpu;
+    if (g && r->win && r->d_win && r->d_counts && r->d_first && parkable(r)) {
+        bool closing;
+        {
+            std::lock_guard<std::mutex> lk(g->life_mu);
+            closing = g->free_requested;
+        }
+        if (!closing) {  // park the window buffers for the next reader on this context
+            free_parked(g);  // the newest window size wins the slot
+            auto& pr = g->parked_reader;
             pr.window = r->window;
             pr.h_win = r->win;
             pr.d_win = r->d_win;
@@ -584,12 +691,14 @@ void reader_release(revel_log_reader* r) {
             r->d_out_cap = 0;
         }
     }
-    if (r->gpu) {
-        if (r->win) revel_gpu_host_free(r->gpu, r->win);
-        revel_gpu_free(r->gpu, r->d_win);
-        revel_gpu_free(r->gpu, r->d_counts);
-        revel_gpu_free(r->gpu, r->d_first);
-        revel_gpu_free(r->gpu, r->d_out);
+    if (g) {
+        if (r->win) revel_gpu_host_free(g, r->win);
+        revel_gpu_free(g, r->d_win);
+        revel_gpu_free(g, r->d_counts);
+        revel_gpu_free(g, r->d_first);
+        revel_gpu_free(g, r->d_out);
+        r->gpu = nullptr;
+        revel::context_unpin(g);  // may destroy a context freed while this reader lived
     }
     revel_sequential_file_free(r->file);
 }
@@ -609,9 +718,15 @@ int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t ini
     *out = nullptr;
     if (!file) return set_error(REVEL_INVALID_ARGUMENT, "null file");
     if (checksum && !gpu) {
-        revel_sequential_file_free(file);
-        return set_error(REVEL_NOT_SUPPORT, "checksum verification runs on the GPU: pass a revel_gpu_context");
+        // Reader::new(file, checksum, initial_offset): verify on the calling
+        // thread's default context (current HIP device); no CPU fallback.
+        int rc = revel::default_context(&gpu);
+        if (rc) {
+            revel_sequential_file_free(file);
+            return rc;
+        }
     }
+    if (gpu) revel::context_pin(gpu);
     auto* r = new revel_log_reader;
     r->file = file;
     r->checksum = checksum != 0;

@@ -130,8 +130,6 @@ __global__ __launch_bounds__(256) void k_scan_apply(const T* __restrict__ in, ui
     }
 }
 
-constexpr int kVerifyThreads = 512;
-constexpr uint32_t kRecCap = 256;  // records per LDS batch per wave
 
 // x^(-8 pad) mod P for pad = 0..3 (x^-1 = (P+1)/x, reflected 0x05EC76F1).
 struct InvPad {
@@ -152,153 +150,6 @@ constexpr InvPad make_inv_pad() {
 static_assert(multmodp(make_inv_pad().v[1], x8n(1)) == 0x80000000u, "x^-8 * x^8 == 1");
 __constant__ InvPad c_inv_pad = make_inv_pad();
 
-struct VerifyWaveLds {
-    uint16_t s[kRecCap];    // start of the CRC range (= header offset + 6)
-    uint16_t em1[kRecCap];  // end of the range minus one (off + 7 + len - 1 <= 32767); s - 1 for bad headers
-    uint32_t acc[kRecCap];  // xor of lane contributions, aligned to E = ceil4(end)
-    uint32_t nrec;
-    uint32_t more_off;
-};
-
-// Per-lane segmented CRC.  Every record's contributions are aligned to its
-// word-aligned range end E = ceil4(e): the lane holding e absorbs the final
-// word with the bytes past e zeroed (that is R * x^(8 pad)), lanes ending
-// earlier shift their partial register by E - chunk_end; the finalizer
-// multiplies by x^(-8 pad).  Records whose header is bad get an empty range.
-__global__ __launch_bounds__(kVerifyThreads) void k_verify_records(const uint8_t* __restrict__ image, uint64_t nbytes,
-                                                                   uint64_t base_offset,
-                                                                   const uint32_t* __restrict__ first,
-                                                                   revel_record_result* __restrict__ out) {
-    constexpr int TM = TM_S2R;
-    __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
-    fill_tables<TM>(tab);
-    __shared__ VerifyWaveLds wl_all[kVerifyThreads / 64];
-    __syncthreads();
-    VerifyWaveLds& wl = wl_all[threadIdx.x >> 6];
-    const LaneConst L = make_lane_const();
-    const uint32_t lane = lane_id();
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    const uint64_t waves_per_wg = kVerifyThreads / 64;
-    const uint64_t gwave = blockIdx.x * waves_per_wg + (threadIdx.x >> 6);
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-
-    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
-        const uint64_t base = b * kBlockSize;
-        const uint8_t* blk = image + base;
-        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
-        const uint32_t cs = lane * 512u, ce = cs + 512u;
-        uint32_t out_base = first[b];
-        uint32_t walk_from = 0;
-        for (;;) {
-            // ---- lane 0 walks up to kRecCap records into LDS ----
-            if (lane == 0) {
-                uint32_t off = walk_from, n = 0, cont = 0xFFFFFFFFu;
-                while (bl - off >= kHeaderSize) {
-                    if (n == kRecCap) { cont = off; break; }
-                    const Hdr h = read_header(blk, off, bl);
-                    const uint32_t st = classify(h, off, bl);
-                    wl.s[n] = (uint16_t)(off + 6);
-                    wl.em1[n] = (uint16_t)(st == REVEL_REC_OK ? off + kHeaderSize + h.len - 1u : off + 5u);
-                    wl.acc[n] = 0;
-                    ++n;
-                    if (st != REVEL_REC_OK) break;
-                    off += kHeaderSize + h.len;
-                }
-                wl.nrec = n;
-                wl.more_off = cont;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t nrec = wl.nrec;
-            const uint32_t cont = wl.more_off;
-
-            // Range of record k as [s, e) with exact e; E = aligned end.
-            // Bad records: s = e (empty).
-            auto load_rec = [&](uint32_t k, uint32_t& s, uint32_t& e, uint32_t& E) {
-                if (k >= nrec) { s = e = E = 0xFFFFFFFFu; return; }
-                s = wl.s[k];
-                e = uint32_t(wl.em1[k]) + 1u;
-                E = (e + 3u) & ~3u;
-            };
-            // first record whose range ends after cs (ranges are increasing)
-            uint32_t lo = 0, hi = nrec;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
-            }
-            uint32_t r = lo, s, e, E;
-            load_rec(r, s, e, E);
-            while (r < nrec && s == e) { ++r; load_rec(r, s, e, E); }
-
-            uint32_t state = 0;
-            if (cs < bl && s < ce) {
-#pragma unroll 2
-                for (uint32_t t = 0; t < 32; ++t) {
-                    const uint32_t p16 = cs + t * 16u;
-                    if (p16 >= bl || s >= ce) break;  // nothing of this batch left in the chunk
-                    const uint4 v = load16_guarded(blk, p16, bl);
-                    if (p16 >= s && p16 + 16u < e) {
-                        state = absorb4<TM>(state, v, L, tab);  // interior: no boundary in these 16 bytes
-                    } else {
-                        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const uint32_t p = p16 + q * 4u;
-                            // keep bytes of [s, e) inside [p, p+4)
-                            const uint32_t lo_b = s > p ? min(s - p, 4u) : 0u;
-                            const uint32_t hi_b = e > p ? min(e - p, 4u) : 0u;
-                            uint32_t keep = hi_b >= 4u ? 0xFFFFFFFFu : ((1u << (8u * hi_b)) - 1u);
-                            keep &= lo_b >= 4u ? 0u : (0xFFFFFFFFu << (8u * lo_b));
-                            state = absorb<TM>(state, ws[q] & keep, L, tab);
-                            if (e > p && e <= p + 4u) {  // record ends in this word: flush
-                                atomicXor(&wl.acc[r], state);
-                                state = 0;
-                                do { ++r; load_rec(r, s, e, E); } while (r < nrec && s == e);
-                            }
-                        }
-                    }
-                }
-                // a record still open at the chunk end: shift to its aligned end
-                if (r < nrec && s < ce && e > ce) {
-                    atomicXor(&wl.acc[r], gf_mul(gf_x8n_block(E - ce), state));
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-
-            // ---- finalize: one lane per record ----
-            for (uint32_t k = lane; k < nrec; k += 64) {
-                const uint32_t off = uint32_t(wl.s[k]) - 6u;
-                const Hdr h = read_header(blk, off, bl);
-                const uint32_t st = classify(h, off, bl);
-                revel_record_result res;
-                res.file_offset = base_offset + base + off;
-                res.length = h.len;
-                res.stored_crc = h.stored;
-                res.type = (uint8_t)h.type;
-                res.reserved[0] = res.reserved[1] = 0;
-                if (st == REVEL_REC_OK) {
-                    const uint32_t n = h.len + 1u;  // type byte + payload
-                    const uint32_t e = off + kHeaderSize + h.len;
-                    const uint32_t pad = ((e + 3u) & ~3u) - e;
-                    const uint32_t raw = gf_mul(c_inv_pad.v[pad], wl.acc[k]);
-                    const uint32_t ix = gf_mul(gf_x8n_block(n), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-                    res.computed_crc = mask(raw ^ ix);
-                    res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
-                } else {
-                    res.computed_crc = 0;
-                    res.status = (uint8_t)st;
-                }
-                out[out_base + k] = res;
-            }
-            out_base += nrec;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (cont == 0xFFFFFFFFu) break;
-            walk_from = cont;
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Config C3, v2: S4R tables, 16 waves/CU, pipelined loads, wave-uniform fast
@@ -1030,212 +881,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
     }
 }
 
-// ---------------------------------------------------------------------------
-// C3 sparse verify, ring experiment (variant 11): v3's per-lane logic over the
-// blocks with at most kListPerBlock records, with the two 128-B rounds as a
-// 16-slot register ring -- a slot is refilled the moment it is consumed, with
-// the data two rounds ahead (this block's rounds 2, 3, then the NEXT block's
-// rounds 0, 1), so ~15 of 16 slots stay in flight across block boundaries
-// instead of v3's one round issued per round.  Same registers, same 16 waves/CU.
-// The next block's list entry / count / output slot are issued before its data.
-// ---------------------------------------------------------------------------
-template <int kRingGroup>
-__global__ __launch_bounds__(kVerify2Threads) void k_verify_records3r(const uint8_t* __restrict__ image,
-                                                                      uint64_t nbytes, uint64_t base_offset,
-                                                                      const uint32_t* __restrict__ first,
-                                                                      revel_record_result* __restrict__ out,
-                                                                      uint32_t lead,
-                                                                      const uint64_t* __restrict__ hlist,
-                                                                      const uint32_t* __restrict__ counts) {
-    __shared__ uint32_t tab[32768];
-    __shared__ VerifyWaveLds2 wl_all[kVerify2Threads / 64];
-    fill_tables<TM_S4R>(tab);
-    __syncthreads();
-    VerifyWaveLds2& wl = wl_all[threadIdx.x >> 6];
-    const LaneConst L = make_lane_const();
-    const uint32_t lane = lane_id();
-    const uint64_t vbytes = nbytes + lead;
-    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;
-    const uint64_t waves_per_wg = kVerify2Threads / 64;
-    const uint64_t nwaves = gridDim.x * waves_per_wg;
-    const uint32_t cs = lane * 512u, ce = cs + 512u;
-    const uint32_t wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    BlockSeq<false> seq(b_lo + blockIdx.x * waves_per_wg + wave_in_wg);
-    uint64_t b = seq.next(counts, nwaves, b_hi);
-    if (b >= b_hi) return;  // wave-uniform
-    uint32_t pf_count = counts[b], pf_first = first[b];
-    // list row base in SGPRs + a 32-bit lane offset (saddr form): a per-lane
-    // 64-bit row pointer held across the loop spilled, and its reload drained the ring
-    auto list_entry_of = [&](uint64_t blk_idx) {
-        const uint64_t* row = hlist + blk_idx * kListStride;
-        uint32_t lo = lane * 8u;
-        asm volatile("" : "+v"(lo));  // keep the compiler from hoisting a 64-bit row + lane pointer
-        return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(row) + lo);
-    };
-    uint64_t pf_hl = list_entry_of(b);
-    uint4 A[8], B[8];
-    // slots refilled together: the group's loads hit the same lane line back to
-    // back (one refill per slot spread a line's 8 accesses over a round, and
-    // with 128 KiB of lines in flight per CU the line left the L1 in between)
-    auto load8 = [&](uint4* v, const uint8_t* p) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ldg4_plain(reinterpret_cast<const uint4*>(p + j * 16));
-    };
-    {
-        const uint8_t* blk0 = image + b * kBlockSize - lead;
-        load8(A, blk0 + cs);
-        load8(B, blk0 + cs + 128);
-    }
-    while (b < b_hi) {
-        const uint64_t base = b * kBlockSize;
-        const uint8_t* blk = image + base - lead;
-        const uint64_t bn = seq.next(counts, nwaves, b_hi);
-        const uint8_t* nblk = bn < b_hi ? image + bn * kBlockSize - lead : blk;  // loads stay unconditional
-        const uint32_t np = min(pf_count, kListPerBlock);
-        const uint32_t out_base = __builtin_amdgcn_readfirstlane(pf_first);
-        {
-            const Hdr h = list_header(pf_hl);
-            const uint32_t sz = lane < np ? kHeaderSize + h.len : 0u;
-            const uint32_t off = wave_exclusive_sum(sz);
-            if (lane < np) {
-                const bool bad = classify(h, off, kBlockSize) != REVEL_REC_OK;
-                wl.off[lane] = (uint16_t)off;
-                wl.s[lane] = bad ? kNoRange : (uint16_t)(off + 6);
-                wl.em1[lane] = bad ? kNoRange : (uint16_t)(off + kHeaderSize + h.len - 1u);
-                wl.acc[lane] = 0;
-                wl.hstored[lane] = h.stored;
-                wl.hlt[lane] = h.len | (h.type << 16);
-            }
-            if (lane == 0) wl.s[np] = wl.em1[np] = kNoRange;
-        }
-        wave_lds_sync();
-        const uint32_t nrec = np;
-        uint32_t lo = 0, hi = nrec;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (uint32_t(wl.em1[mid]) + 1u > cs) hi = mid; else lo = mid + 1;
-        }
-        uint32_t r = lo, s = wl.s[r], e = uint32_t(wl.em1[r]) + 1u;
-        // the finalizer's table lookups are issued here, behind this block's
-        // rounds 0, 1 and ahead of every refill: issued after the refills,
-        // waiting for them would drain the ring
-        uint32_t xo;  // x^(8(e - ce)) of the record open at the chunk end (if any)
-        {
-            lo = r, hi = nrec;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (uint32_t(wl.em1[mid]) + 1u > ce) hi = mid; else lo = mid + 1;
-            }
-            const uint32_t so = wl.s[lo], eo = uint32_t(wl.em1[lo]) + 1u;
-            const bool open = lo < nrec && so < ce && eo > ce;
-            xo = g_x8n_tab[open ? eo - ce : 0u];
-        }
-        // (a bad header's length can exceed the table: only in-block lengths index it)
-        const uint32_t ln = lane < nrec ? wl.hlt[lane] & 0xFFFFu : kBlockSize;
-        const uint32_t ix = g_init_xor_tab[ln < kBlockSize ? ln + 1u : 0u];
-        uint32_t state = 0;
-        auto consume = [&](const uint4 v, const uint32_t p16) {
-            const bool interior = (p16 + 16u <= s) || (p16 >= s && p16 + 16u < e);
-            if (__all(interior)) {
-                state = p16 == s ? 0u : state;
-                state = absorb4<TM_S4R>(state, v, L, tab);
-            } else {
-                // rolled: 32 slots are unrolled, the boundary path is kept small
-#pragma unroll 1
-                for (uint32_t q = 0; q < 4; ++q) {
-                    const uint32_t p = p16 + q * 4u;
-                    const uint32_t w = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
-                    if (s >= p + 4u) {
-                    } else if (e > p + 4u) {
-                        if (s >= p) state = 0;
-                        const uint32_t lb = s > p ? s - p : 0u;
-                        state = absorb<TM_S4R>(state, w & (0xFFFFFFFFu << (8u * lb)), L, tab);
-                    } else if (e > p) {
-                        if (s >= p) state = 0;
-                        const uint32_t lb = s > p ? s - p : 0u;
-                        const uint32_t hb = e - p;
-                        if (lb == 0 && hb == 4) {
-                            state = absorb<TM_S4R>(state, w, L, tab);
-                        } else {
-                            for (uint32_t t = lb; t < hb; ++t)
-                                state = byte_step_s4r(state, (w >> (8u * t)) & 0xffu, L, tab);
-                        }
-                        atomicXor(&wl.acc[r], state);
-                        state = 0;
-                        ++r;
-                        s = wl.s[r];
-                        e = uint32_t(wl.em1[r]) + 1u;
-                    }
-                }
-            }
-        };
-        // rounds 0, 1 of this block are in A, B; each consumed slot is refilled
-        // two rounds ahead
-#pragma unroll
-        for (int g = 0; g < 8; g += kRingGroup) {
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j) consume(A[j], cs + j * 16);
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j)
-                A[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + 256 + j * 16));
-        }
-#pragma unroll
-        for (int g = 0; g < 8; g += kRingGroup) {
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j) consume(B[j], cs + 128 + j * 16);
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j)
-                B[j] = ldg4_plain(reinterpret_cast<const uint4*>(blk + cs + 384 + j * 16));
-        }
-        // the next block's list before its data (loads complete in order)
-        if (bn < b_hi) {
-            pf_count = counts[bn];
-            pf_first = first[bn];
-            pf_hl = list_entry_of(bn);
-        }
-#pragma unroll
-        for (int g = 0; g < 8; g += kRingGroup) {
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j) consume(A[j], cs + 256 + j * 16);
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j)
-                A[j] = ldg4_plain(reinterpret_cast<const uint4*>(nblk + cs + j * 16));
-        }
-#pragma unroll
-        for (int g = 0; g < 8; g += kRingGroup) {
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j) consume(B[j], cs + 384 + j * 16);
-#pragma unroll
-            for (int j = g; j < g + kRingGroup; ++j)
-                B[j] = ldg4_plain(reinterpret_cast<const uint4*>(nblk + cs + 128 + j * 16));
-        }
-        if (r < nrec && s < ce && e > ce) atomicXor(&wl.acc[r], gf_mul(xo, state));
-        wave_lds_sync();
-        if (lane < nrec) {
-            const uint32_t off = wl.off[lane];
-            const Hdr h{wl.hstored[lane], wl.hlt[lane] & 0xFFFFu, wl.hlt[lane] >> 16};
-            const uint32_t st = classify(h, off, kBlockSize);
-            revel_record_result res;
-            res.file_offset = base_offset + base - lead + off;
-            res.length = h.len;
-            res.stored_crc = h.stored;
-            res.type = (uint8_t)h.type;
-            res.reserved[0] = res.reserved[1] = 0;
-            if (st == REVEL_REC_OK) {
-                res.computed_crc = mask(wl.acc[lane] ^ ix);
-                res.status = res.computed_crc == res.stored_crc ? REVEL_REC_OK : REVEL_REC_BAD_CHECKSUM;
-            } else {
-                res.computed_crc = 0;
-                res.status = (uint8_t)st;
-            }
-            out[out_base + lane] = res;
-        }
-        wave_lds_sync();
-        b = bn;
-    }
-}
 
-#include "verify5.inc"
 #include "verify_dense.inc"
 #include "verify_rows.inc"
 constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
@@ -1435,17 +1081,42 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
 // sparse partial blocks through the single-wave verify2 launch.  Each kernel
 // skips the others' blocks by count.  Lists: verify = hlist + overflow entries
 // in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
-template <bool FRAME, bool SPARSE_V5 = false, bool TQ = false, bool R64 = false, int RING = 0, bool TQ8 = false,
-          bool ROWS = false>
+// The blocks the sparse-block kernels leave: every block with more than
+// kListPerBlock records (partial first / last ones too) through
+// k_verify_records_dense, then the sparse partial blocks through the
+// single-wave verify2 launch.  Each kernel skips the others' blocks by count.
+template <bool FRAME>
+static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes,
+                                           uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                           uint32_t lead, const uint64_t* hl, const uint32_t* d_counts,
+                                           const uint64_t* xl, uint32_t xs, hipStream_t st) {
+    const uint64_t vbytes = nbytes + lead;
+    const uint64_t nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t waves = kDenseThreads / 64;
+    const uint32_t grid =
+        (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
+    hipLaunchKernelGGL(k_verify_records_dense<FRAME>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
+                       d_first, d_out, lead, hl, d_counts, xl, xs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || (lead == 0 && vbytes % kBlockSize == 0)) return e;
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st, img,
+                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs);
+    return hipGetLastError();
+}
+
+// Verify (or FRAME: append framing) split by block density, from the
+// per-block record counts.  Production (ROWS): the whole blocks with
+// 1..kListPerBlock records are listed (k_sparse_blocks) and verified by
+// k_verify_rows; !ROWS = v3 over those blocks (experiments only, with its
+// TQ / R64 / TQ8 load shapes).  Lists: verify = hlist + overflow entries in the
+// result slots (xlist = out, 3 u64 apart); FRAME = framing list.
+template <bool FRAME, bool ROWS = true, bool TQ = false, bool R64 = false, bool TQ8 = false>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
                                       hipStream_t st, uint32_t* d_blist = nullptr) {
     const uint64_t vbytes = nbytes + lead;
-    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize, nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
-    auto grid_for = [&](uint64_t n, uint64_t waves) {
-        return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + waves - 1) / waves));
-    };
+    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;
     if (b_hi > b_lo) {
         if constexpr (ROWS) {
             // qualifying blocks listed first (d_blist[0] = count, then the list)
@@ -1459,151 +1130,66 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL((k_verify_rows<FRAME, kRowsRing>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + 1, d_blist);
-        } else if constexpr (SPARSE_V5) {
-            static_assert(!FRAME, "v5 verifies only");
-            hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(b_hi, kV5Threads / 64)), dim3(kV5Threads), 0, st, img,
-                               nbytes, base_offset, d_first, d_out, hl, d_counts);
-        } else if constexpr (RING != 0) {
-            static_assert(!FRAME, "ring experiment verifies only");
-            hipLaunchKernelGGL(k_verify_records3r<RING>, dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
-                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
-                               d_counts);
         } else {
-            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE, TQ, R64, TQ8>), dim3(grid_for(b_hi - b_lo, kVerify2Threads / 64)),
+            const uint64_t waves = kVerify2Threads / 64;
+            const uint32_t grid = (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>((uint64_t)di.num_cu, (b_hi - b_lo + waves - 1) / waves));
+            hipLaunchKernelGGL((k_verify_records3<FRAME, SEL_SPARSE, TQ, R64, TQ8>), dim3(grid),
                                dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, lead, hl,
                                d_counts, xl, xs);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_verify_records_dense<FRAME>, dim3(grid_for(nblocks, kDenseThreads / 64)), dim3(kDenseThreads),
-                       0, st, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || (lead == 0 && vbytes % kBlockSize == 0)) return e;
-    hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st, img,
-                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs);
-    return hipGetLastError();
+    return launch_dense_and_partial<FRAME>(di, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, st);
 }
 
 // the dense kernel reads aligned 16 B relative to the image start
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-template <bool FRAME, int BP>
-static hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes,
-                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                 uint32_t lead, const uint64_t* hl, const uint32_t* d_counts, hipStream_t st) {
-    hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_WHOLE>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
-                       img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts,
-                       reinterpret_cast<const uint64_t*>(d_out), 3u);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !partial) return e;
-    hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img, nbytes,
-                       base_offset, d_first, d_out, lead, hl, d_counts, reinterpret_cast<const uint64_t*>(d_out), 3u);
-    return hipGetLastError();
-}
 
 // The qualifying-block list of verify lives after the header lists (hlist_words).
 static uint32_t* block_list(const uint64_t* hl, uint64_t nblocks) {
     return reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(hl) + nblocks * kListStride);
 }
 
-hipError_t verify_records_variant(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes,
-                                  uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                                  const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
+// Production verify paths (test hook `path`): 0 = production -- with the
+// count pass's header lists and a 16-B aligned image, the density split
+// (k_verify_rows + dense + partial), else v3 over every block; 1 = v3 forced
+// to walk the headers itself (a verify without its count pass); 2 = v3 with
+// the header lists (the unaligned-image path).  Experiment arms live in
+// tools/experiments (x_records.hip).
+hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_image, uint64_t nbytes,
+                               uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                               const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
+    if (path < 0 || path > 2) return hipErrorInvalidValue;
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    if (variant == 1) {
-        const uint64_t waves = kVerifyThreads / 64;
-        const uint64_t grid =
-            std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 2, (nblocks + waves - 1) / waves));
-        hipLaunchKernelGGL(k_verify_records, dim3((uint32_t)grid), dim3(kVerifyThreads), 0, st,
-                           static_cast<const uint8_t*>(d_image), nbytes, base_offset, d_first, d_out);
-        return hipGetLastError();
-    }
     hipError_t e0 = ensure_len_tables(di, st);
     if (e0 != hipSuccess) return e0;
     const uint64_t waves = kVerify2Threads / 64;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
-    const uint64_t* hl = variant == 2 ? nullptr : d_hlist;
+    const uint64_t* hl = path == 1 ? nullptr : d_hlist;
+    const uint32_t* counts = path == 1 ? nullptr : d_counts;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
-    if (hl && d_counts) {
+    if (hl && counts) {
         // list the headers of blocks with more than kListCap records
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
-        hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
+        hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, counts, d_first, hl,
                            d_out);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     const bool partial = nbytes % kBlockSize != 0;
-    switch (variant) {
-        case 3: return launch_verify2<false, BP_MASK>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                      d_counts, st);
-        case 4: return launch_verify2<false, BP_MASK_NOVOTE>(grid, partial, img, nbytes, base_offset, d_first, d_out,
-                                                             0u, hl, d_counts, st);
-        case 5:  // round-1 production: one kernel for whole and partial blocks
-            hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
-                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                               reinterpret_cast<const uint64_t*>(d_out), 3u);
-            return hipGetLastError();
-        case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
-                                                       hl, d_counts, st);
-        case 7:
-            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
-            return launch_verify_split<false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                                                    reinterpret_cast<const uint64_t*>(d_out),
-                                                    (uint32_t)(sizeof(revel_record_result) / 8), st);
-        case 9:  // experiment: split with quad-coalesced loads + DPP transpose in v3
-            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
-            return launch_verify_split<false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                           d_counts, reinterpret_cast<const uint64_t*>(d_out),
-                                                           (uint32_t)(sizeof(revel_record_result) / 8), st);
-        case 10:  // control for 9: the same 64-B rounds with lane-owned loads
-            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
-            return launch_verify_split<false, false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                                                  d_counts, reinterpret_cast<const uint64_t*>(d_out),
-                                                                  (uint32_t)(sizeof(revel_record_result) / 8), st);
-        case 14:  // experiment: variant 9's quad transpose with 128-B rounds
-            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
-            return launch_verify_split<false, false, true, false, 0, true>(
-                di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                reinterpret_cast<const uint64_t*>(d_out), (uint32_t)(sizeof(revel_record_result) / 8), st);
-        case 11:  // experiments: sparse blocks through the 16-slot ring kernel,
-        case 12:  // slots refilled in groups of 4 (11), 8 (12), 2 (13)
-        case 13: {
-            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
-            const uint64_t* xl = reinterpret_cast<const uint64_t*>(d_out);
-            const uint32_t xs = (uint32_t)(sizeof(revel_record_result) / 8);
-            if (variant == 11)
-                return launch_verify_split<false, false, false, false, 4>(di, img, nbytes, base_offset, d_first,
-                                                                          d_out, 0u, hl, d_counts, xl, xs, st);
-            if (variant == 12)
-                return launch_verify_split<false, false, false, false, 8>(di, img, nbytes, base_offset, d_first,
-                                                                          d_out, 0u, hl, d_counts, xl, xs, st);
-            return launch_verify_split<false, false, false, false, 2>(di, img, nbytes, base_offset, d_first, d_out,
-                                                                      0u, hl, d_counts, xl, xs, st);
-        }
-        case 15:  // session-5 production: v3 over the sparse whole blocks
-            if (!(hl && d_counts && aligned16(img))) return hipErrorInvalidValue;
-            return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                                              reinterpret_cast<const uint64_t*>(d_out),
-                                              (uint32_t)(sizeof(revel_record_result) / 8), st);
-        case 0:
-            if (hl && d_counts && aligned16(img))
-                return launch_verify_split<false, false, false, false, 0, false, true>(
-                    di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
-                    reinterpret_cast<const uint64_t*>(d_out), (uint32_t)(sizeof(revel_record_result) / 8), st,
-                    block_list(hl, nblocks));
-            [[fallthrough]];
-        case 8:  // session-2 production: v3 over every whole block
-        case 2: return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
-                                             d_counts, st);
-        default: return hipErrorInvalidValue;
-    }
+    if (path == 0 && hl && counts && aligned16(img))
+        return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts,
+                                          reinterpret_cast<const uint64_t*>(d_out),
+                                          (uint32_t)(sizeof(revel_record_result) / 8), st, block_list(hl, nblocks));
+    return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts, st);
 }
 
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                           const uint32_t* d_counts, hipStream_t st) {
-    return verify_records_variant(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
+    return verify_records_path(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
 }
 
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
@@ -1649,7 +1235,7 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
     const bool partial = lead != 0 || (image_len + lead) % kBlockSize != 0;
     const bool lists = d_counts && d_first && d_xlist;
     if (lists && aligned16(d_image) && d_blist)
-        return launch_verify_split<true, false, false, false, 0, false, true>(
+        return launch_verify_split<true>(
             di, static_cast<const uint8_t*>(d_image), image_len, 0ull, d_first, nullptr, lead, nullptr, d_counts,
             d_xlist, 1u, st, d_blist);
     return launch_verify3<true>(grid, partial, static_cast<const uint8_t*>(d_image), image_len, 0ull,

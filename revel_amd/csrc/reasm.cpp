@@ -18,7 +18,8 @@ extern "C" int revel_gpu_reassemble(revel_gpu_context* ctx, const void* d_image,
     *payload_bytes = 0;
     if (nphys == 0) return REVEL_OK;
     if (!d_image || !d_phys || !d_out || !d_payload) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    if (hipSetDevice(ctx->di.device) != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return set_error(REVEL_IO_ERROR, "hipSetDevice failed");
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const uint64_t n = nphys;
     const uint64_t tiles = revel::scan_scratch_words(n);

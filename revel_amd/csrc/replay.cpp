@@ -22,6 +22,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <thread>
 #include <vector>
@@ -218,7 +219,8 @@ int replay(revel_gpu_context* ctx, uint64_t length, uint64_t base_offset, int mo
         return set_error(REVEL_INVALID_ARGUMENT, "bad replay mode %d", mode);
     if (base_offset % REVEL_BLOCK_SIZE)
         return set_error(REVEL_INVALID_ARGUMENT, "replay must start on a block boundary");
-    TRY(hipSetDevice(ctx->di.device), "hipSetDevice");
+    revel::DeviceGuard guard(ctx->di.device);
+    TRY(guard.err(), "hipSetDevice");
     memset(out, 0, sizeof *out);
     out->first_bad_offset = UINT64_MAX;
     NodeBinding near_gpu(ctx->di.device);  // before the ring: its pinned pages land on the GPU's node
@@ -302,7 +304,7 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
         return set_error(REVEL_INVALID_ARGUMENT, "range [%llu, +%llu) past the end of %s", (unsigned long long)offset,
                          (unsigned long long)length, path);
     }
-    bool io_error = false;
+    std::atomic<bool> io_error{false};
     int rc;
     if (io == REVEL_REPLAY_IO_MMAP) {
         // offset is block- (hence page-) aligned; the io threads copy straight
@@ -331,7 +333,7 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
                             if (r < 0 && errno == EINTR) continue;
                             if (r <= 0) {
                                 memset(dst + done, 0, n - done);
-                                io_error = true;
+                                io_error.store(true, std::memory_order_relaxed);
                                 return;
                             }
                             done += (uint64_t)r;
@@ -339,7 +341,7 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
                     });
     }
     ::close(fd);
-    if (rc == REVEL_OK && io_error) return set_error(REVEL_IO_ERROR, "short read from %s", path);
+    if (rc == REVEL_OK && io_error.load()) return set_error(REVEL_IO_ERROR, "short read from %s", path);
     return rc;
 }
 

@@ -98,7 +98,12 @@ class GpuContext:
     def stream(self) -> int:
         return lib().revel_gpu_context_stream(self._h)
 
+    def trim(self) -> None:
+        """Drop the window buffers parked by freed readers (revel_gpu_context_trim)."""
+        check(lib().revel_gpu_context_trim(self.handle))
+
     def close(self) -> None:
+        """revel_gpu_context_free: deferred to the last reader still using it."""
         if self._h:
             lib().revel_gpu_context_free(self._h)
             self._h = None
@@ -167,9 +172,12 @@ class GpuContext:
         check(lib().revel_gpu_synth_full_blocks(self._h, blocks.ptr, nblocks, seed, first, None))
 
     def verify_image(self, image: DeviceBuffer, nbytes: int, base_offset: int = 0,
-                     variant: Optional[int] = None) -> np.ndarray:
+                     variant: Optional[int] = None, path: Optional[int] = None) -> np.ndarray:
         """Config C3: walk + CRC every physical record of a device-resident
-        WAL image.  Returns a structured array (RECORD_DTYPE) in file order."""
+        WAL image.  Returns a structured array (RECORD_DTYPE) in file order.
+        path: a production verify path of the test hook (0 = production, 1 =
+        header walk without the count pass's lists, 2 = v3 with the lists);
+        variant: an experiment arm of tools/experiments."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
         if image.nbytes < nbytes:
@@ -184,11 +192,15 @@ class GpuContext:
         tail_count = self.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         total = int(tail_first) + int(tail_count)
         out = self.alloc(max(1, total) * RECORD_DTYPE.itemsize)
-        if variant is None:
-            check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
+        if variant is not None:
+            from ._lib import experiments  # kernel variants kept for the record (tools/experiments)
+            check(experiments().revel_x_verify_records_variant(self._h, variant, image.ptr, nbytes, base_offset,
+                                                               first.ptr, out.ptr, None))
+        elif path is not None:
+            check(L.revel_gpu_verify_records_path(self._h, path, image.ptr, nbytes, base_offset, first.ptr, out.ptr,
+                                                  None))
         else:
-            check(L.revel_gpu_verify_records_variant(self._h, variant, image.ptr, nbytes, base_offset, first.ptr,
-                                                     out.ptr, None))
+            check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
         self.sync()
         res = self.d2h(out, total * RECORD_DTYPE.itemsize, np.uint8).view(RECORD_DTYPE)
         return res

@@ -9,7 +9,9 @@ Mirrors the reference names and semantics:
   returns the logical record's bytes, ``None`` at EOF (the reference returns an
   empty Slice, log_reader.rs:140), and raises ``RevelError(IOError)`` on a
   checksum mismatch (log_reader.rs:142-152).  With ``checksum=True`` the CRCs
-  are verified on the GPU (a :class:`revel_amd.gpu.GpuContext` is required).
+  are verified on the GPU: ``gpu``'s, or without one the calling thread's
+  default context on its current device (the reference's 3-argument
+  ``Reader::new(file, checksum, initial_offset)``, log_reader.rs:62).
 """
 from __future__ import annotations
 

@@ -1,0 +1,43 @@
+"""The kernel arms kept for the record in tools/experiments/libexperiments.so
+(not the product): each must still equal the oracle, so the numbers in
+profiles/ and DESIGN.md section 4 stay reproducible.  One pass over the golden
+images and one corrupted Zipf image per arm; the production paths get the
+full parity suite in test_gpu.py."""
+import numpy as np
+import pytest
+
+from conftest import golden_image
+from oracle import oracle_c as oc
+from test_gpu import compare_walk, kat_blocks, run_full, zipf_image
+
+pytestmark = pytest.mark.gpu
+
+C3_ARMS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15]
+C2_ARMS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 20, 21, 22]  # 100-106: read-ceiling shapes, no CRC
+
+
+@pytest.mark.parametrize("variant", C3_ARMS)
+def test_c3_verify_arm_vs_oracle(gpu_ctx, golden_index, variant):
+    for name in golden_index:
+        img = golden_image(name)
+        dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=variant), oc.walk(img))
+    rng = np.random.default_rng(13)
+    img = bytearray(oc.write_image(zipf_image(rng, 4 << 20)))
+    ref = oc.walk(bytes(img))
+    for v in rng.choice(np.flatnonzero(ref["length"] > 0), 30, replace=False):
+        img[int(ref["file_offset"][v]) + 7 + int(rng.integers(0, int(ref["length"][v])))] ^= 4
+    img = bytes(img)
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=variant), oc.walk(img))
+
+
+@pytest.mark.parametrize("variant", C2_ARMS)
+def test_c2_crc_arm_vs_oracle(gpu_ctx, variant):
+    blocks = kat_blocks()
+    rng = np.random.default_rng(variant)
+    extra = rng.integers(0, 256, (300, blocks.shape[1]), dtype=np.uint8)
+    extra[:, 4], extra[:, 5], extra[:, 6] = 0xF9, 0x7F, 1
+    blocks = np.vstack([blocks, extra])
+    got, _ = run_full(gpu_ctx, blocks, variant=variant)
+    assert np.array_equal(got, oc.full_block_crcs(blocks))

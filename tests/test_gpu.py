@@ -145,15 +145,19 @@ def compare_walk(res, ref):
         assert np.array_equal(res[f].astype(np.uint64), ref[f].astype(np.uint64)), f
 
 
-VERIFY_VARIANTS = [0, 15, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14]
+# Production verify paths (test hook): 0 = production (density split:
+# k_verify_rows + dense + partial), 1 = v3 walking the headers itself (verify
+# without its count pass), 2 = v3 with the header lists (unaligned images).
+# The experiment arms are checked in test_experiments_gpu.py.
+VERIFY_PATHS = [0, 1, 2]
 
 
-@pytest.mark.parametrize("variant", VERIFY_VARIANTS)
-def test_verify_golden_images(gpu_ctx, golden_index, variant):
+@pytest.mark.parametrize("path", VERIFY_PATHS)
+def test_verify_golden_images(gpu_ctx, golden_index, path):
     for name in golden_index:
         img = golden_image(name)
         dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-        res = gpu_ctx.verify_image(dimg, len(img), variant=variant)
+        res = gpu_ctx.verify_image(dimg, len(img), path=path)
         compare_walk(res, oc.walk(img))
 
 
@@ -170,8 +174,8 @@ def zipf_image(rng, nbytes_target):
     return recs
 
 
-@pytest.mark.parametrize("variant", VERIFY_VARIANTS)
-def test_verify_zipf_and_corruption(gpu_ctx, variant):
+@pytest.mark.parametrize("path", VERIFY_PATHS)
+def test_verify_zipf_and_corruption(gpu_ctx, path):
     rng = np.random.default_rng(13)
     recs = zipf_image(rng, 16 << 20)
     img = bytearray(oc.write_image(recs))
@@ -184,21 +188,21 @@ def test_verify_zipf_and_corruption(gpu_ctx, variant):
         img[off] ^= 1 << int(rng.integers(0, 8))
     img = bytes(img)
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    res = gpu_ctx.verify_image(dimg, len(img), base_offset=0, variant=variant)
+    res = gpu_ctx.verify_image(dimg, len(img), base_offset=0, path=path)
     ref2 = oc.walk(img)
     compare_walk(res, ref2)
     assert sorted(np.flatnonzero(res["status"] == 1).tolist()) == sorted(victims.tolist())
 
 
-@pytest.mark.parametrize("variant", VERIFY_VARIANTS)
+@pytest.mark.parametrize("path", VERIFY_PATHS)
 @pytest.mark.parametrize("cut", [1, 3, 6, 7, 8, 100, 32767, 32769, 40000])
-def test_verify_partial_last_block(gpu_ctx, cut, variant):
+def test_verify_partial_last_block(gpu_ctx, cut, path):
     rng = np.random.default_rng(cut)
     recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 9000, 30)]
     img = oc.write_image(recs)
     img = img[:min(len(img), cut + 65536)]
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=variant), oc.walk(img))
+    compare_walk(gpu_ctx.verify_image(dimg, len(img), path=path), oc.walk(img))
 
 
 def test_verify_small_records_dense(gpu_ctx):
@@ -208,8 +212,8 @@ def test_verify_small_records_dense(gpu_ctx):
     recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 40, 20000)]
     img = oc.write_image(recs)
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    for v in VERIFY_VARIANTS:
-        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), oc.walk(img))
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), oc.walk(img))
 
 
 @pytest.mark.parametrize("rec_len", [24, 100, 124, 200])
@@ -239,8 +243,8 @@ def test_verify_multi_batch_lists(gpu_ctx, rec_len):
     img = bytes(img)
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
     ref2 = oc.walk(img)
-    for v in VERIFY_VARIANTS:
-        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref2)
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref2)
     assert (ref2["status"] == 1).sum() > 10
 
 
@@ -259,8 +263,8 @@ def test_verify_batch_start_on_16_byte_boundary(gpu_ctx):
         img = oc.write_image(recs)
         dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
         ref = oc.walk(img)
-        for v in VERIFY_VARIANTS:
-            compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref)
+        for v in VERIFY_PATHS:
+            compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)
 
 
 def _density_mix(seed, tail):
@@ -300,25 +304,22 @@ def test_verify_mixed_density(gpu_ctx, tail):
     ref = oc.walk(img)
     assert (ref["status"] == 1).sum() > 10
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
-    for v in (0, 15, 7, 8, 9, 11):
-        compare_walk(gpu_ctx.verify_image(dimg, len(img), variant=v), ref)
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)
 
 
 @pytest.mark.parametrize("shift", [1, 4, 8, 12, 16])
 def test_verify_unaligned_image_base(gpu_ctx, shift):
     """An image that does not start on a 16-B boundary: the split path reads
-    aligned 16 B relative to the image, so such images take the previous
-    kernels (variant 0 falls back, variant 7 refuses); results unchanged."""
+    aligned 16 B relative to the image, so such images take v3 (path 0 falls
+    back to path 2); results unchanged."""
     img = _density_mix(11, "dense")
     buf = gpu_ctx.alloc(len(img) + 64)
     gpu_ctx.h2d(buf, np.frombuffer(img, dtype=np.uint8), dst_offset=shift)
     view = _View(buf, shift, len(img))
     ref = oc.walk(img)
-    for v in (0, 8):
-        compare_walk(gpu_ctx.verify_image(view, len(img), variant=v), ref)
-    if shift % 16:
-        with pytest.raises(RevelError):
-            gpu_ctx.verify_image(view, len(img), variant=7)
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(view, len(img), path=v), ref)
 
 
 def test_verify_base_offset_and_random_bytes(gpu_ctx):
@@ -755,7 +756,7 @@ def test_property_random_streams_vs_oracle(gpu_ctx):
 def test_property_dense_streams_vs_oracle(gpu_ctx):
     """Hypothesis: dense streams (hundreds to thousands of small records, so
     blocks hold several header-list batches), a periodic tail that puts batch
-    starts on fixed alignments, optional bit flips -> every verify variant and
+    starts on fixed alignments, optional bit flips -> every verify path and
     the device append framing (at a random block offset) equal the oracle."""
     from hypothesis import HealthCheck, given, settings
     from hypothesis import strategies as hs
@@ -775,8 +776,8 @@ def test_property_dense_streams_vs_oracle(gpu_ctx):
         img = bytes(img)
         d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
         ref = oc.walk(img)
-        for v in VERIFY_VARIANTS:
-            compare_walk(gpu_ctx.verify_image(d, len(img), variant=v), ref)
+        for v in VERIFY_PATHS:
+            compare_walk(gpu_ctx.verify_image(d, len(img), path=v), ref)
         blob = np.frombuffer(b"".join(recs) or b"\0", dtype=np.uint8)
         dp = gpu_ctx.upload(blob)
         fimg, fn, _ = gpu_ctx.append_records(dp, [len(r) for r in recs], block_offset)
@@ -863,3 +864,160 @@ def test_reader_parked_window_buffers(gpu_ctx, golden_index):
             rc = log.Reader(env.MemorySequentialFile(golden_image(a)), checksum=True, gpu=gpu_ctx, window_bytes=window)
             assert read(rc) == want[a], (a, window)
             del rc
+
+
+# ---- the reference's own vectors through the HIP kernels ----
+def _kat():
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "kat.json")) as f:
+        return json.load(f)
+
+
+def kat_records_image(lead=0):
+    """The five RFC 3720 B.4 vectors of crc.rs:50-76 framed as physical
+    records: type byte = the vector's first byte, payload = the rest, so the
+    record CRC crc32c(type || payload) (log_writer.rs:107-111) IS the vector's
+    published CRC.  `lead` bytes of a zero-filled FULL record come first, to
+    move the vectors across lane / row positions of the verify kernel."""
+    import struct
+    img = b""
+    if lead:
+        pad = bytes(lead)
+        img += struct.pack("<IHB", po.mask(oc.extend(1, pad)), len(pad), 1) + pad
+    want = []
+    for v in _kat()["value"]:
+        d = bytes.fromhex(v["data_hex"])
+        want.append((len(img), v["crc"]))
+        img += struct.pack("<IHB", po.mask(v["crc"]), len(d) - 1, d[0]) + d[1:]
+    return img, want
+
+
+@pytest.mark.parametrize("lead", [0, 1, 9, 57, 1000, 32768 - 7 - 206 - 7])
+def test_rfc3720_kats_through_verify_kernel(gpu_ctx, lead):
+    img, want = kat_records_image(lead)
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    res = gpu_ctx.verify_image(dimg, len(img))
+    got = {int(r["file_offset"]): r for r in res}
+    for off, kat_crc in want:
+        r = got[off]
+        assert int(r["computed_crc"]) == po.mask(kat_crc), (lead, off)
+        assert po.unmask(int(r["computed_crc"])) == kat_crc
+        assert int(r["status"]) == 0
+    compare_walk(res, oc.walk(img))
+
+
+ISCSI_HEX = "01c000000000000000000000000000001400000000000400000000140000001828000000000000000200000000000000"
+
+
+def test_iscsi_pdu_and_hello_world_through_append_reader_verify(gpu_ctx):
+    """crc.rs:66-74's 48-byte iSCSI PDU starts with 0x01 (FULL): appended as a
+    47-byte record on the device, its stored header must be
+    mask(0xd9963a56) LE, len 47, type 1; the GPU verify and the GPU-verified
+    reader (explicit and default context) must accept it.  Same for the
+    hello-world image of log_reader.rs:231."""
+    pdu = bytes.fromhex(ISCSI_HEX)
+    assert pdu[0] == 1
+    hello_img = bytes(_kat()["hello_world_image"])
+    for payload, kat_crc, golden in [(pdu[1:], 0xD9963A56, None), (b"hello world", None, hello_img)]:
+        d = gpu_ctx.upload(np.frombuffer(payload, dtype=np.uint8))
+        img_d, n, bo = gpu_ctx.append_records(d, [len(payload)], 0)
+        img = gpu_ctx.d2h(img_d, n).tobytes()
+        assert n == 7 + len(payload) and bo == n
+        stored = int.from_bytes(img[:4], "little")
+        if kat_crc is not None:
+            assert stored == po.mask(kat_crc)
+        if golden is not None:
+            assert img == golden
+        assert img[4:7] == bytes([len(payload) & 0xFF, len(payload) >> 8, 1])
+        res = gpu_ctx.verify_image(img_d, n)
+        assert len(res) == 1 and int(res["computed_crc"][0]) == stored and int(res["status"][0]) == 0
+        for ctx in (gpu_ctx, None):
+            rd = log.Reader(env.MemorySequentialFile(img), True, 0, gpu=ctx)
+            assert list(rd) == [payload]
+
+
+# ---- the drop-in: caller files + the 3-argument Reader::new ----
+class _PySeq:
+    def __init__(self, data, chunk=1 << 30):
+        self.data, self.pos, self.chunk = data, 0, chunk
+
+    def read(self, n):
+        d = self.data[self.pos:self.pos + min(n, self.chunk)]
+        self.pos += len(d)
+        return d
+
+    def skip(self, n):
+        self.pos += n
+
+
+def test_three_arg_reader_callbacks_every_golden(golden_index):
+    """Reader::new(Box<dyn SequentialFile>, true, 0) (log_reader.rs:62): a
+    caller-implemented file, checksum on, NO explicit context -- the thread's
+    default context verifies on the GPU -- for every golden image."""
+    for name in sorted(golden_index):
+        img = golden_image(name)
+        for chunk in (1 << 30, 4096):
+            rd = log.Reader(env.CallbackSequentialFile(_PySeq(img, chunk)), True, 0)
+            try:
+                got = list(rd)
+            except RevelError as e:
+                assert e.code == IO_ERROR
+                got = "error"
+            try:
+                want = po.read_all(img, checksum=True)
+            except po.CorruptionError:
+                want = "error"
+            assert got == want, (name, chunk)
+
+
+def test_callback_writer_then_three_arg_reader_roundtrip():
+    """Writer::new(Rc<RefCell<dyn WritableFile>>) on a caller file, read back
+    through Reader::new(file, true, initial_offset) with GPU verification."""
+    class W:
+        def __init__(self):
+            self.b = bytearray()
+
+        def append(self, d):
+            self.b += d
+
+        def flush(self):
+            pass
+
+        def close(self):
+            pass
+
+        def sync(self):
+            pass
+    rng = np.random.default_rng(99)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 100000, 50)]
+    w = W()
+    wr = log.Writer(env.CallbackWritableFile(w))
+    for r in recs:
+        wr.add_record(r)
+    img = bytes(w.b)
+    assert img == oc.write_image(recs)
+    for off in (0, 40000, len(img) // 2):
+        rd = log.Reader(env.CallbackSequentialFile(_PySeq(img, 10000)), True, off)
+        assert drain(rd.read_record) == drain(po.LogReader(img, True, off).read_record), off
+
+
+def test_context_freed_before_its_reader():
+    """revel_gpu_context_free while a reader still uses the context defers
+    the release to the reader's free (was a use-after-free)."""
+    from revel_amd import gpu as G
+    rng = np.random.default_rng(5)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 70000, 30)]
+    img = oc.write_image(recs)
+    for _ in range(3):
+        ctx = G.GpuContext(0)
+        rd = log.Reader(env.MemorySequentialFile(img), checksum=True, gpu=ctx, window_bytes=65536)
+        first = rd.read_record()
+        ctx.close()  # deferred: the reader pins the context
+        assert [first] + list(rd) == recs
+        del rd  # the last reader's release destroys the context
+    ctx = G.GpuContext(0)
+    rd = log.Reader(env.MemorySequentialFile(img), checksum=True, gpu=ctx)
+    assert list(rd) == recs
+    assert ctx.trim() is None
+    del rd
+    ctx.close()

@@ -223,3 +223,139 @@ def test_property_writer_and_host_reader_vs_oracle():
         assert drain(rd.read_record) == drain(po.LogReader(img, False, off).read_record)
 
     prop()
+
+
+# ---- caller-implemented files (the drop-in for dyn WritableFile / SequentialFile) ----
+
+class PyWritable:
+    """A caller's `dyn WritableFile` (env.rs:40-50), kept by the caller (the
+    Rc<RefCell<..>> clone db.rs:56-63 holds to sync the log)."""
+
+    def __init__(self, fail_after=None):
+        self.data = bytearray()
+        self.calls = []
+        self.fail_after = fail_after
+
+    def append(self, d):
+        if self.fail_after is not None and len(self.data) + len(d) > self.fail_after:
+            raise OSError("disk full")
+        self.data += d
+        self.calls.append("append")
+
+    def flush(self):
+        self.calls.append("flush")
+
+    def close(self):
+        self.calls.append("close")
+
+    def sync(self):
+        self.calls.append("sync")
+
+
+class PySequential:
+    """A caller's `Box<dyn SequentialFile>` (env.rs:52-57) returning short
+    reads of at most `chunk` bytes."""
+
+    def __init__(self, data, chunk=1 << 30):
+        self.data, self.pos, self.chunk = data, 0, chunk
+
+    def read(self, n):
+        d = self.data[self.pos:self.pos + min(n, self.chunk)]
+        self.pos += len(d)
+        return d
+
+    def skip(self, n):
+        self.pos += n
+
+
+def test_callback_writer_reproduces_every_golden_image(golden_index):
+    from tests_gen import edge_records
+    for name, ent in golden_index.items():
+        recs = edge_records(name)
+        f = PyWritable()
+        w = log.Writer(env.CallbackWritableFile(f), ent["block_offset"])
+        for r in recs:
+            w.add_record(r)
+        if ent["post"] is None:
+            assert hashlib.sha256(bytes(f.data)).hexdigest() == ent["sha256"], name
+        else:
+            assert bytes(f.data) == po.write_image(recs, ent["block_offset"]), name
+    # hello world (log_reader.rs:231): header, payload, flush per record (log_writer.rs:114-119)
+    f = PyWritable()
+    w = log.Writer(env.CallbackWritableFile(f))
+    w.add_record(b"hello world")
+    assert bytes(f.data) == golden_image("hello_world")
+    assert f.calls == ["append", "append", "flush"]
+
+
+def test_callback_writer_shared_file_sync_and_errors():
+    f = PyWritable(fail_after=100)
+    wf = env.CallbackWritableFile(f)
+    w = log.Writer(wf)
+    w.add_record(b"x" * 50)
+    wf.sync()  # the DB's own clone syncs the shared file (db.rs:109-111)
+    assert f.calls[-1] == "sync"
+    with pytest.raises(RevelError) as e:
+        w.add_record(b"y" * 100)  # append raises OSError -> io::Error -> IOError (error.rs:25-29)
+    assert e.value.code == _lib.IO_ERROR
+    wf.close()
+    assert f.calls[-1] == "close"
+
+
+def test_callback_writer_release_and_required_append():
+    import ctypes
+    L = revel_amd.lib()
+    h = ctypes.c_void_p()
+    rc = L.revel_writable_file_from_callbacks(None, _lib.APPEND_FN(), _lib.FILE_OP_FN(), _lib.FILE_OP_FN(),
+                                              _lib.FILE_OP_FN(), _lib.RELEASE_FN(), ctypes.byref(h))
+    assert rc == _lib.INVALID_ARGUMENT and not h.value
+    before = len(env._owned)
+    f = env.CallbackWritableFile(PyWritable())
+    assert len(env._owned) == before + 1
+    f.free()  # release drops the caller's object (the Rc clone)
+    assert len(env._owned) == before
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 4096, 1 << 30])
+def test_callback_reader_nochecksum_short_reads(chunk):
+    rng = np.random.default_rng(11)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 90000, 12)]
+    img = oc.write_image(recs)
+    before = len(env._owned)
+    rd = log.Reader(env.CallbackSequentialFile(PySequential(img, chunk)), checksum=False, window_bytes=65536)
+    assert list(rd) == recs
+    del rd  # the reader owns the file: releasing it drops the caller's object
+    assert len(env._owned) == before
+
+
+def test_callback_reader_initial_offset_with_and_without_skip():
+    recs = [bytes([i]) * 20000 for i in range(10)]
+    img = oc.write_image(recs)
+    for off in [0, 20007, 40000, len(img)]:
+        want = po.read_all(img, checksum=False, initial_offset=off)
+        for skip in (True, False):
+            rd = log.Reader(env.CallbackSequentialFile(PySequential(img, 5000), skip=skip), checksum=False,
+                            initial_offset=off)
+            assert list(rd) == want, (off, skip)
+
+
+def test_callback_reader_read_error_is_ioerror():
+    class Broken(PySequential):
+        def read(self, n):
+            raise OSError("EIO")
+    rd = log.Reader(env.CallbackSequentialFile(Broken(b"")), checksum=False)
+    with pytest.raises(RevelError) as e:
+        rd.read_record()
+    assert e.value.code == _lib.IO_ERROR
+
+
+def test_three_arg_reader_fails_loudly_without_gpu():
+    """Reader::new(file, checksum=true, 0) with no context: the thread's
+    default context needs a gfx950 device -- NOT_SUPPORT, no CPU fallback."""
+    if gpu.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    before = len(env._owned)
+    with pytest.raises(RevelError) as e:
+        log.Reader(env.CallbackSequentialFile(PySequential(golden_image("hello_world"))), True, 0)
+    assert e.value.code == _lib.NOT_SUPPORT
+    assert len(env._owned) == before  # the file was consumed and released

@@ -18,7 +18,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from revel_amd import BLOCK_SIZE, env, gpu, log  # noqa: E402
-from revel_amd._lib import check, lib  # noqa: E402
+from revel_amd._lib import check, experiments, lib  # noqa: E402
 
 
 def make_image(target: int, seed: int = 0x5EED0003) -> bytes:
@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=1 << 30, help="size of the written Zipf image")
     ap.add_argument("--tile", type=int, default=4, help="repeat the image's whole blocks this many times")
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--variants", default="0,3,4")
+    ap.add_argument("--variants", default="0,15")
     ap.add_argument("--image", choices=["zipf", "full"], default="zipf",
                     help="full = C2-style full blocks (1 record/block): the verify kernels' base cost")
     a = ap.parse_args()
@@ -87,7 +87,11 @@ def main():
             check(L.revel_gpu_count_records(ctx.handle, d.ptr, n, counts.ptr, None))
             check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
             e1.record()
-            check(L.revel_gpu_verify_records_variant(ctx.handle, variant, d.ptr, n, 0, first.ptr, out.ptr, None))
+            if variant == 0:  # production, from the product library
+                check(L.revel_gpu_verify_records(ctx.handle, d.ptr, n, 0, first.ptr, out.ptr, None))
+            else:  # experiment arms (tools/experiments/libexperiments.so)
+                check(experiments().revel_x_verify_records_variant(ctx.handle, variant, d.ptr, n, 0, first.ptr,
+                                                                   out.ptr, None))
             e2.record()
             ctx.sync()
             times_all.append(e0.elapsed_ms(e2))

@@ -1,0 +1,153 @@
+// x_records.hip -- config C3 verify EXPERIMENT arms (not part of librevel_wal.so).
+//
+// This translation unit compiles the production k_records.hip (its kernels,
+// tables and launchers) together with the verify kernels measured on the way
+// to the production k_verify_rows: the round-1 kernel (v1), v2's boundary
+// paths, v3's load shapes (quad transpose, 64-B rounds), v5 and the register
+// ring.  Results: profiles/r1*_c3_*.txt, r2_c3_v7_vs_v3.txt; DESIGN.md section
+// 4.2.  Symbols are hidden except revel_x_verify_records_variant; the device
+// tables are this module's own copies (filled by its own k_init_len_tables).
+#include "k_records.hip"
+
+namespace {
+#include "x_verify_v1.inc"
+#include "x_verify_ring.inc"
+#include "x_verify5.inc"
+}  // namespace
+
+namespace revel {
+namespace {
+
+template <bool FRAME, int BP>
+hipError_t launch_verify2(uint64_t grid, bool partial, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
+                          const uint32_t* d_first, revel_record_result* d_out, uint32_t lead, const uint64_t* hl,
+                          const uint32_t* d_counts, hipStream_t st) {
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_WHOLE>), dim3((uint32_t)grid), dim3(kVerify2Threads), 0, st,
+                       img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts,
+                       reinterpret_cast<const uint64_t*>(d_out), 3u);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !partial) return e;
+    hipLaunchKernelGGL((k_verify_records2<FRAME, BP, BS_PARTIAL>), dim3(1), dim3(kVerify2Threads), 0, st, img, nbytes,
+                       base_offset, d_first, d_out, lead, hl, d_counts, reinterpret_cast<const uint64_t*>(d_out), 3u);
+    return hipGetLastError();
+}
+
+uint32_t grid_for(const DeviceInfo& di, uint64_t n, uint64_t waves) {
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + waves - 1) / waves));
+}
+
+hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                    const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
+                    const uint32_t* d_counts, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    if (variant == 1) {
+        hipLaunchKernelGGL(k_verify_records, dim3(std::max<uint32_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 2,
+                                                                                     (nblocks + 7) / 8))),
+                           dim3(kVerifyThreads), 0, st, img, nbytes, base_offset, d_first, d_out);
+        return hipGetLastError();
+    }
+    if (variant == 0) return verify_records_path(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
+    if (variant == 2) return verify_records_path(di, 1, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
+    if (variant == 8) return verify_records_path(di, 2, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
+    hipError_t e0 = ensure_len_tables(di, st);
+    if (e0 != hipSuccess) return e0;
+    const uint64_t grid = grid_for(di, nblocks, kVerify2Threads / 64);
+    const uint64_t* hl = d_hlist;
+    if (hl && d_counts) {
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
+        hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
+                           d_out);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    const bool partial = nbytes % kBlockSize != 0;
+    const bool lists = hl && d_counts && aligned16(img);
+    const uint64_t* xl = reinterpret_cast<const uint64_t*>(d_out);
+    const uint32_t xs = (uint32_t)(sizeof(revel_record_result) / 8);
+    const uint64_t b_hi = nbytes / kBlockSize;
+    switch (variant) {
+        case 3: return launch_verify2<false, BP_MASK>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                      d_counts, st);
+        case 4: return launch_verify2<false, BP_MASK_NOVOTE>(grid, partial, img, nbytes, base_offset, d_first, d_out,
+                                                             0u, hl, d_counts, st);
+        case 5:  // round-1 production: one kernel for whole and partial blocks
+            hipLaunchKernelGGL((k_verify_records2<false, BP_BYTES, BS_ALL>), dim3((uint32_t)grid),
+                               dim3(kVerify2Threads), 0, st, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                               xl, 3u);
+            return hipGetLastError();
+        case 6: return launch_verify2<false, BP_BYTES>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u,
+                                                       hl, d_counts, st);
+        case 7: {  // v5 over the sparse whole blocks
+            if (!lists) return hipErrorInvalidValue;
+            if (b_hi) {
+                hipLaunchKernelGGL(k_verify_records5, dim3(grid_for(di, b_hi, kV5Threads / 64)), dim3(kV5Threads), 0,
+                                   st, img, nbytes, base_offset, d_first, d_out, hl, d_counts);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl,
+                                                   xs, st);
+        }
+        case 9:  // v3 split with quad-coalesced loads + DPP transpose
+            if (!lists) return hipErrorInvalidValue;
+            return launch_verify_split<false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                           d_counts, xl, xs, st);
+        case 10:  // control for 9: the same 64-B rounds with lane-owned loads
+            if (!lists) return hipErrorInvalidValue;
+            return launch_verify_split<false, false, false, true>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl,
+                                                                  d_counts, xl, xs, st);
+        case 14:  // variant 9's quad transpose with 128-B rounds
+            if (!lists) return hipErrorInvalidValue;
+            return launch_verify_split<false, false, true, false, true>(di, img, nbytes, base_offset, d_first, d_out,
+                                                                        0u, hl, d_counts, xl, xs, st);
+        case 15:  // session-5 production: v3 over the sparse whole blocks
+            if (!lists) return hipErrorInvalidValue;
+            return launch_verify_split<false, false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
+                                                     xl, xs, st);
+        case 11:  // 16-slot ring, slots refilled in groups of 4 (11), 8 (12), 2 (13)
+        case 12:
+        case 13: {
+            if (!lists) return hipErrorInvalidValue;
+            if (b_hi) {
+                const uint32_t g = grid_for(di, b_hi, kVerify2Threads / 64);
+                if (variant == 11)
+                    hipLaunchKernelGGL(k_verify_records3r<4>, dim3(g), dim3(kVerify2Threads), 0, st, img, nbytes,
+                                       base_offset, d_first, d_out, 0u, hl, d_counts);
+                else if (variant == 12)
+                    hipLaunchKernelGGL(k_verify_records3r<8>, dim3(g), dim3(kVerify2Threads), 0, st, img, nbytes,
+                                       base_offset, d_first, d_out, 0u, hl, d_counts);
+                else
+                    hipLaunchKernelGGL(k_verify_records3r<2>, dim3(g), dim3(kVerify2Threads), 0, st, img, nbytes,
+                                       base_offset, d_first, d_out, 0u, hl, d_counts);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl,
+                                                   xs, st);
+        }
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+}  // namespace revel
+
+// Verify variant `variant` (numbering of DESIGN.md section 4.2) on a product
+// context; uses the header lists of the context's last count pass when they
+// belong to this image, like revel_gpu_verify_records.
+extern "C" __attribute__((visibility("default"))) int revel_x_verify_records_variant(
+    revel_gpu_context* ctx, int variant, const void* d_image, size_t nbytes, uint64_t base_offset,
+    const uint32_t* d_first, revel_record_result* d_out, void* stream) {
+    if (!ctx || !d_image || !d_first || !d_out) return REVEL_INVALID_ARGUMENT;
+    if (nbytes == 0) return REVEL_OK;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = revel::x_verify(ctx->di, variant, d_image, nbytes, base_offset, d_first, d_out,
+                                   memo ? ctx->hlist : nullptr, memo ? ctx->hlist_counts : nullptr, st);
+    ctx->hlist_image = nullptr;
+    if (e == hipErrorInvalidValue) return REVEL_INVALID_ARGUMENT;
+    return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
