@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
     ap.add_argument("--e2e-gib", type=float, default=4.0,
-                    help="per-rank host-RAM replay size for the end_to_end field (0 = skip)")
+                    help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
     return ap.parse_args()
@@ -89,19 +89,36 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+PROD_KERNEL = "k_full_blocks4<1024, false>"  # the production C2 kernel (k_blocks.hip)
+
+
+def library_sha256() -> str:
+    import hashlib
+    from revel_amd._lib import LIB_PATH
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def pmc_traffic(nblocks: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass, if one was
-    taken for this workload (profiles/pmc_c2.json, written by
-    tools/pmc_summary.py), else None."""
+    """HBM bytes per launch from the committed rocprofv3 PMC pass
+    (profiles/pmc_c2.json, written by tools/pmc_summary.py) -- only when that
+    pass measured THIS build: same kernel symbol, same librevel_wal.so
+    SHA-256, same block count.  Returns (bytes or None, source note)."""
     path = os.path.join(ROOT, "profiles", "pmc_c2.json")
     try:
         with open(path) as f:
             p = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no PMC pass committed (profiles/pmc_c2.json)"
+    if p.get("kernel") != PROD_KERNEL:
+        return None, f"PMC pass was of {p.get('kernel')!r}, not the production {PROD_KERNEL!r}"
+    if p.get("library_sha256") != library_sha256():
+        return None, "PMC pass was taken on another build of librevel_wal.so"
     if int(p.get("blocks", -1)) != nblocks:
-        return None
-    return p.get("hbm_bytes_per_launch")
+        return None, f"PMC pass was over {p.get('blocks')} blocks, not {nblocks}"
+    return p.get("hbm_bytes_per_launch"), (f"profiles/pmc_c2.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                                           f"of {PROD_KERNEL} on this librevel_wal.so "
+                                           f"(sha256 {p['library_sha256'][:12]}), gfx950 FETCH_SIZE x2")
 
 
 def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
@@ -215,25 +232,71 @@ def c1_reference_path(oracle_c):
 
 
 def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
-    """PCIe-inclusive rate (not `value`): every rank replays `gib` GiB of its
-    blocks from a pageable host-RAM image through the pinned ring -> H2D ->
-    verify pipeline (revel_gpu_replay_memory), all ranks started together;
-    rate = total bytes / max-over-ranks pipeline time (ring allocation excluded)."""
+    """Config C5, PCIe-inclusive (not `value`): ONE WAL file on the host holds
+    every rank's blocks (rank r's `gib` GiB at offset r * gib); each rank loads
+    its block-aligned shard of it onto its GPU (revel_gpu_wal_shard_load: mmap
+    of the file -> 8 fill threads -> 3 x 64 MiB pinned ring -> H2D on a copy
+    stream, records counted as each window lands -> verify of the resident
+    shard), the ranks exchange their boundary blobs and rank 0 stitches them
+    (revel_wal_stitch_new).  Rate = file bytes / max-over-ranks load time;
+    file writing is outside the clock.  The file was just written, so it is
+    read from the page cache."""
+    import tempfile
+    from revel_amd import shard
     k = min(nblocks, int(gib * (1 << 30)) // BLOCK_SIZE)
-    host = ctx.d2h(dblocks, k * BLOCK_SIZE)              # host image = the first k device blocks
+    per = k * BLOCK_SIZE
+    total = per * D.world
+    d = os.environ.get("REVEL_BENCH_DIR") or tempfile.gettempdir()
+    path = os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{os.getppid() if D.world > 1 else os.getpid()}.log")
+    if D.rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(total)
     D.barrier()
-    st = ctx.replay_memory(host, full_blocks=True, window_bytes=64 << 20, nbuffers=4, io_threads=8)
+    host = ctx.d2h(dblocks, per)  # this rank's part of the WAL = its first k device blocks
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        view = memoryview(host)
+        done = 0
+        while done < per:
+            done += os.pwrite(fd, view[done:], D.rank * per + done)
+    finally:
+        os.close(fd)
+    del host
     D.barrier()
-    wall_max = D.max(st["seconds"])   # pipeline clock: first window read -> last verdict (ring set up before)
-    bad = D.sum(float(st["bad"]))
+    s, e = shard.block_ranges(total, D.world)[D.rank]
+    t0 = time.perf_counter()
+    sh = shard.WalShard(ctx, s, e - s, path=path, file_bytes=total, checksum=True, read=False,
+                        window_bytes=64 << 20, io_threads=8)
+    t_load = time.perf_counter() - t0
+    info = sh.info()
+    blob = sh.boundary()
+    sh.close()
+    wall_max = D.max(t_load)
+    blobs = [blob]
+    if D.dist:
+        blobs = [None] * D.world
+        D.dist.all_gather_object(blobs, blob)
+    D.barrier()
+    if D.rank == 0:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+    summ = shard.Stitch(blobs).summary() if D.rank == 0 else {}
     return {
         "unit": "GiB/s",
-        "value": round(k * BLOCK_SIZE * D.world / 2**30 / wall_max, 2),
-        "per_rank_GiB": round(k * BLOCK_SIZE / 2**30, 2),
-        "h2d_GiB_s_rank0": round(k * BLOCK_SIZE / 2**30 / (st["h2d_ms"] / 1e3), 2),
-        "bad_blocks": int(bad),
-        "path": "pageable host RAM -> 8 memcpy threads -> 4 x 64 MiB pinned ring -> H2D (copy stream) -> "
-                "C2 verify (compute stream) -> 24 B summary D2H per window",
+        "value": round(total / 2**30 / wall_max, 2),
+        "file_GiB": round(total / 2**30, 2),
+        "per_rank_GiB": round(per / 2**30, 2),
+        "h2d_GiB_s_rank0": round((e - s) / 2**30 / (info["h2d_ms"] / 1e3), 2) if info["h2d_ms"] else None,
+        "read_s_rank0": round(info["read_seconds"], 3),
+        "verify_ms_rank0": round(info["kernel_ms"], 3),
+        "physical_records": summ.get("physical"),
+        "bad_records": summ.get("bad"),
+        "stitched": summ.get("stitched"),
+        "source": f"one WAL file in {d} (page cache: written just before), shared by all ranks",
+        "path": "file mmap -> 8 fill threads -> 3 x 64 MiB pinned ring -> H2D (copy stream) + per-window record count "
+                "-> verify of the HBM-resident shard -> boundary blob -> rank-0 stitch",
     }
 
 
@@ -291,7 +354,8 @@ def c3_records(ctx, D, gib: float, iters: int = 5):
         "physical_records_rank0": nphys,
         "bad_records": int(bad),
         "alg_GB_s_rank0": round((n + 24 * nphys) / (ms / 1e3) / 1e9, 1),
-        "path": "count (per-block header walk + header list) -> scan -> verify (production: v3 over blocks with <= 64 records, one lane per record over denser blocks)",
+        "path": "count (per-block header walk + header list) -> scan -> verify (production: k_verify_rows over blocks "
+                "with <= 64 records, k_verify_records_dense over denser ones, single-wave partial blocks)",
         "data": "Zipf(1.1) 64 B..32 KiB records framed on device by revel_gpu_append_records",
     }
 
@@ -339,7 +403,7 @@ def main():
     value = total_blocks * BLOCK_SIZE / 2**30 / (wall / args.steps)
     alg_bytes = n * (BLOCK_SIZE + 4 + 1)          # read block, write masked CRC + ok flag
     achieved = alg_bytes / (kern_ms_max / 1e3) / 1e9
-    traffic = pmc_traffic(n)
+    traffic, traffic_source = pmc_traffic(n)
 
     e2e = None
     if args.e2e_gib > 0:
@@ -383,6 +447,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "kernel_ms": round(kern_ms_max, 4),
                 "alg_bytes_per_launch": alg_bytes,
             },

@@ -204,7 +204,11 @@ typedef struct revel_record_result {
  * FULL record of 32761 bytes.  d_masked_out[b] = mask(crc32c(block[6:32768]))
  * = the value log_writer.rs:107-111 stores for that payload;
  * d_ok[b] = (stored == computed && length == 32761 && type == FULL).
- * d_ok may be NULL.  Asynchronous on `stream` (NULL = context stream). */
+ * d_ok may be NULL.  Asynchronous on `stream` (NULL = context stream).
+ * Alignment: any d_blocks is accepted and gives the same results; the
+ * kernel's 16-byte loads run at full rate only when d_blocks is 16-byte
+ * aligned (every revel_gpu_malloc / hipMalloc pointer is), an unaligned base
+ * splits them (tests/test_gpu.py test_full_blocks_unaligned_base). */
 int revel_gpu_crc_full_blocks(revel_gpu_context* ctx, const void* d_blocks, size_t nblocks,
                               uint32_t* d_masked_out, uint8_t* d_ok, void* stream);
 
@@ -379,6 +383,95 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
                           size_t window_bytes, int nbuffers, int io_threads, revel_replay_stats* out);
 int revel_gpu_replay_memory(revel_gpu_context* ctx, const uint8_t* image, uint64_t length, uint64_t base_offset,
                             int mode, size_t window_bytes, int nbuffers, int io_threads, revel_replay_stats* out);
+
+/* ---- one WAL across several GPUs (config C5 on N GPUs) ----
+ * Physical records never cross a 32 KiB block (log_writer.rs:66-76), so a WAL
+ * splits into contiguous block-aligned shards that are verified (and
+ * reassembled) independently, one per GPU, with no collective.  Only logical
+ * records whose fragments span a shard boundary need the neighbours: each
+ * shard keeps its boundary records (the leading MIDDLE/LAST run and the open
+ * FIRST MIDDLE* tail), and a host stitch folds them in file order with the
+ * reader's rules (log_reader.rs:95-129, LevelDB-correct as the replay reader).
+ * In one process revel_gpu_replay_sharded drives n contexts on n host threads;
+ * with one process per GPU each rank loads its shard, exports its boundary
+ * (revel_wal_shard_boundary) and one rank stitches the gathered blobs. */
+typedef struct revel_wal_shard revel_wal_shard;
+/* offsets[0..n]: n contiguous block-aligned ranges covering [0, file_bytes)
+ * (offsets[k+1] - offsets[k] = shard k's bytes; trailing shards may be empty). */
+int revel_wal_shard_ranges(uint64_t file_bytes, int n, uint64_t* offsets);
+#define REVEL_SHARD_VERIFY 0  /* load + verify every physical record, boundary records kept */
+#define REVEL_SHARD_READ 1    /* + device reassembly: logical records and their payloads in HBM */
+typedef struct revel_wal_shard_info {
+    int device;
+    int checksum;
+    uint64_t offset, length;     /* the shard's byte range of the WAL */
+    uint64_t file_bytes;         /* the WAL's size (torn-tail rule at its end) */
+    uint64_t physical, bad;      /* physical records verified / not REVEL_REC_OK */
+    uint64_t events, records;    /* READ: shard-local events (revel_gpu_reassemble), records among them */
+    uint64_t payload_bytes;      /* READ: gathered payload bytes of those records */
+    const void* d_image;         /* the shard's bytes in HBM (library-owned) */
+    const revel_record_result* d_phys;
+    const revel_logical_record* d_events;  /* READ */
+    const void* d_payload;       /* READ */
+    double seconds;              /* host wall time of the load (read + H2D + verify [+ reassembly]) */
+    double read_seconds;         /* summed host time filling pinned windows */
+    double h2d_ms, kernel_ms;    /* summed H2D time / verify (+ reassembly) time, HIP events */
+} revel_wal_shard_info;
+/* Loads bytes [offset, offset + length) of the WAL at `path` (mmap'd; or of
+ * the host `image` holding the whole WAL when path is NULL) into HBM of ctx's
+ * device: io_threads fill a ring of pinned windows (window_bytes, 0 = 64 MiB),
+ * each is copied on a copy stream and its records counted on the context
+ * stream as it lands; then every physical record is verified (and with
+ * REVEL_SHARD_READ reassembled) on the device.  offset must be block-aligned
+ * and offset + length a block multiple or file_bytes.  The shard pins ctx. */
+int revel_gpu_wal_shard_load(revel_gpu_context* ctx, const char* path, const uint8_t* image, uint64_t file_bytes,
+                             uint64_t offset, uint64_t length, int checksum, int flags, size_t window_bytes,
+                             int io_threads, revel_wal_shard** out);
+int revel_wal_shard_info_get(const revel_wal_shard* s, revel_wal_shard_info* out);
+/* The shard's boundary as a self-contained blob (records + their payloads
+ * with REVEL_SHARD_READ): with buf NULL, *n = the size needed. */
+int revel_wal_shard_boundary(const revel_wal_shard* s, uint8_t* buf, size_t cap, size_t* n);
+void revel_wal_shard_free(revel_wal_shard* s);
+/* The same boundary blob from a host header walk of the WAL bytes in host
+ * memory (image = the whole WAL), for a Reader with checksum == false: no
+ * CRC, no GPU (the CPU side of the one-process-per-GPU stitch, and its tests). */
+int revel_wal_shard_boundary_host(const uint8_t* image, uint64_t file_bytes, uint64_t offset, uint64_t length,
+                                  int flags, uint8_t* buf, size_t cap, size_t* n);
+
+/* Host stitch of n shards' boundary blobs, in file order (contiguous). */
+typedef struct revel_wal_stitch revel_wal_stitch;
+typedef struct revel_wal_summary {
+    uint64_t bytes;          /* WAL bytes covered */
+    uint64_t physical, bad;  /* physical records verified / not REVEL_REC_OK */
+    uint64_t records;        /* READ: logical records a Reader returns, stitched ones included */
+    uint64_t errors;         /* READ: Err(IOError) events a Reader returns */
+    uint64_t payload_bytes;  /* READ: their payload bytes; VERIFY: those of the stitched records only */
+    uint64_t stitched;       /* logical records assembled across shard boundaries */
+    double seconds;          /* revel_gpu_replay_sharded: wall time of the parallel loads + stitch */
+} revel_wal_summary;
+int revel_wal_stitch_new(const uint8_t* const* blobs, const size_t* sizes, int n, revel_wal_stitch** out);
+int revel_wal_stitch_summary(const revel_wal_stitch* st, revel_wal_summary* out);
+/* Stitched record i: header offset of its FIRST, payload (host, valid while
+ * the stitch lives; NULL in VERIFY mode), and `before_shard` = the shard whose
+ * own events it precedes in file order. */
+int revel_wal_stitch_record(const revel_wal_stitch* st, size_t i, uint64_t* file_offset, const uint8_t** data,
+                            uint64_t* n, int* before_shard);
+void revel_wal_stitch_free(revel_wal_stitch* st);
+
+/* One process, n GPUs: shard the WAL (revel_wal_shard_ranges), load shard k on
+ * ctxs[k] on its own host thread, stitch.  With REVEL_SHARD_READ,
+ * revel_sharded_replay_next then returns the logical records in file order
+ * exactly as Reader::read_record would (log_reader.rs:76-153): REVEL_OK with
+ * the payload (valid until the next call), REVEL_IO_ERROR for an error event
+ * (continue calling), REVEL_OK with *data NULL at the end. */
+typedef struct revel_sharded_replay revel_sharded_replay;
+int revel_gpu_replay_sharded(revel_gpu_context* const* ctxs, int n, const char* path, const uint8_t* image,
+                             uint64_t file_bytes, int checksum, int flags, size_t window_bytes, int io_threads,
+                             revel_sharded_replay** out);
+int revel_sharded_replay_summary(const revel_sharded_replay* r, revel_wal_summary* out);
+const revel_wal_shard* revel_sharded_replay_shard(const revel_sharded_replay* r, int k);
+int revel_sharded_replay_next(revel_sharded_replay* r, const uint8_t** data, size_t* n, uint64_t* file_offset);
+void revel_sharded_replay_free(revel_sharded_replay* r);
 
 #ifdef __cplusplus
 }

@@ -43,6 +43,27 @@ class ReplayStats(Structure):
 
 
 REPLAY_RECORDS, REPLAY_FULL_BLOCKS = 0, 1
+SHARD_VERIFY, SHARD_READ = 0, 1
+
+
+class ShardInfo(Structure):
+    _fields_ = [("device", c_int), ("checksum", c_int), ("offset", c_uint64), ("length", c_uint64),
+                ("file_bytes", c_uint64), ("physical", c_uint64), ("bad", c_uint64), ("events", c_uint64),
+                ("records", c_uint64), ("payload_bytes", c_uint64), ("d_image", c_void_p), ("d_phys", c_void_p),
+                ("d_events", c_void_p), ("d_payload", c_void_p), ("seconds", ctypes.c_double),
+                ("read_seconds", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class WalSummary(Structure):
+    _fields_ = [("bytes", c_uint64), ("physical", c_uint64), ("bad", c_uint64), ("records", c_uint64),
+                ("errors", c_uint64), ("payload_bytes", c_uint64), ("stitched", c_uint64),
+                ("seconds", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 REPLAY_IO = {"mmap": 0x00, "pread": 0x10, "direct": 0x20}
 
 
@@ -130,6 +151,25 @@ SIGNATURES = {
                                       POINTER(ReplayStats)]),
     "revel_gpu_replay_memory": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_int, c_size_t, c_int, c_int,
                                         POINTER(ReplayStats)]),
+    "revel_wal_shard_ranges": (c_int, [c_uint64, c_int, c_void_p]),
+    "revel_gpu_wal_shard_load": (c_int, [c_void_p, c_char_p, c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_int,
+                                         c_size_t, c_int, POINTER(c_void_p)]),
+    "revel_wal_shard_info_get": (c_int, [c_void_p, POINTER(ShardInfo)]),
+    "revel_wal_shard_boundary": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_size_t)]),
+    "revel_wal_shard_free": (None, [c_void_p]),
+    "revel_wal_shard_boundary_host": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_void_p, c_size_t,
+                                              POINTER(c_size_t)]),
+    "revel_wal_stitch_new": (c_int, [c_void_p, c_void_p, c_int, POINTER(c_void_p)]),
+    "revel_wal_stitch_summary": (c_int, [c_void_p, POINTER(WalSummary)]),
+    "revel_wal_stitch_record": (c_int, [c_void_p, c_size_t, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_uint64),
+                                        POINTER(c_int)]),
+    "revel_wal_stitch_free": (None, [c_void_p]),
+    "revel_gpu_replay_sharded": (c_int, [c_void_p, c_int, c_char_p, c_void_p, c_uint64, c_int, c_int, c_size_t, c_int,
+                                         POINTER(c_void_p)]),
+    "revel_sharded_replay_summary": (c_int, [c_void_p, POINTER(WalSummary)]),
+    "revel_sharded_replay_shard": (c_void_p, [c_void_p, c_int]),
+    "revel_sharded_replay_next": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t), POINTER(c_uint64)]),
+    "revel_sharded_replay_free": (None, [c_void_p]),
 }
 
 # exported test hook (not part of the public header): production verify paths

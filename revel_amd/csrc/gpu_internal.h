@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <mutex>
+#include <vector>
 
 #include "revel_wal.h"
 
@@ -60,6 +61,9 @@ hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phy
 hipError_t reasm_emit(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
                       int checksum, const uint32_t* d_flag, const uint32_t* d_idx, const uint64_t* d_off,
                       const uint32_t* d_end, revel_logical_record* d_out, uint64_t* d_frag_dst, hipStream_t st);
+// *d_ok (zeroed by the caller) += events with status REVEL_LOGICAL_OK.
+hipError_t count_ok_events(const DeviceInfo& di, const revel_logical_record* d_ev, uint64_t n, uint64_t* d_ok,
+                           hipStream_t st);
 hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t image_base,
                         const revel_record_result* d_phys, uint64_t n, const uint64_t* d_frag_dst, void* d_payload,
                         hipStream_t st);
@@ -145,6 +149,17 @@ struct DeviceScratch {
         return e;
     }
 };
+
+// Device reassembly of d_phys's events (revel_gpu_reassemble with the torn-
+// tail rule at image_end); synchronises st.
+hipError_t reassemble_events(revel_gpu_context* ctx, const void* d_image, uint64_t image_base, uint64_t image_end,
+                             const revel_record_result* d_phys, uint64_t n, int checksum, revel_logical_record* d_out,
+                             void* d_payload, uint64_t* nlogical, uint64_t* payload_bytes, hipStream_t st);
+
+// Host header walk without CRC (a Reader with checksum == false): every
+// physical record of img[0, n) (whole blocks from file offset base), statuses
+// as the device walk's other than BAD_CHECKSUM (computed_crc = 0).
+void host_walk(const uint8_t* img, size_t n, uint64_t base, std::vector<revel_record_result>& out);
 
 // Set the thread-local error string; returns code.
 int set_error(int code, const char* fmt, ...);

@@ -571,6 +571,10 @@ constexpr size_t kDefaultWindow = 64u << 20;
 
 // Host-side header walk without CRC (checksum == false): same rules as the
 // device walk so statuses other than BAD_CHECKSUM are identical.
+}  // namespace
+
+namespace revel {
+
 void host_walk(const uint8_t* img, size_t n, uint64_t base, std::vector<revel_record_result>& out) {
     out.clear();
     for (size_t b = 0; b < n; b += REVEL_BLOCK_SIZE) {
@@ -600,6 +604,10 @@ void host_walk(const uint8_t* img, size_t n, uint64_t base, std::vector<revel_re
         }
     }
 }
+
+}  // namespace revel
+
+namespace {
 
 int gpu_verify_window(revel_log_reader* r) {
     revel_gpu_context* g = r->gpu;
@@ -646,7 +654,7 @@ int load_window(revel_log_reader* r) {
     if (got < r->window) r->file_eof = true;
     if (got == 0) return REVEL_OK;
     if (r->gpu && r->checksum) return gpu_verify_window(r);
-    host_walk(r->win, r->win_len, r->win_file_off, r->recs);
+    revel::host_walk(r->win, r->win_len, r->win_file_off, r->recs);
     return REVEL_OK;
 }
 

@@ -169,9 +169,34 @@ __global__ void k_reasm_gather(const uint8_t* __restrict__ image, uint64_t image
     }
 }
 
+// Events with status REVEL_LOGICAL_OK among n (the rest are errors): one
+// atomic add per workgroup into *ok (zeroed by the caller).
+__global__ __launch_bounds__(256) void k_count_ok_events(const revel_logical_record* __restrict__ ev, uint64_t n,
+                                                         unsigned long long* __restrict__ ok) {
+    __shared__ unsigned long long part[256];
+    unsigned long long c = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        c += ev[i].status == REVEL_LOGICAL_OK ? 1u : 0u;
+    part[threadIdx.x] = c;
+    __syncthreads();
+    for (uint32_t s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && part[0]) atomicAdd(ok, part[0]);
+}
+
 }  // namespace
 
 namespace revel {
+hipError_t count_ok_events(const DeviceInfo& di, const revel_logical_record* d_ev, uint64_t n, uint64_t* d_ok,
+                           hipStream_t st) {
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 4, (n + 255) / 256));
+    hipLaunchKernelGGL(k_count_ok_events, dim3((uint32_t)grid), dim3(256), 0, st, d_ev, n,
+                       reinterpret_cast<unsigned long long*>(d_ok));
+    return hipGetLastError();
+}
+
 hipError_t reasm_classify(const DeviceInfo& di, const revel_record_result* d_phys, uint64_t n, uint64_t image_end,
                           int checksum, uint32_t* d_flag, uint64_t* d_len, uint32_t* d_end, hipStream_t st) {
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 8, (n + 255) / 256));

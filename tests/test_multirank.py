@@ -1,9 +1,11 @@
 """World-size-2 gloo tests of the multi-GPU path on the CPU.
 
-Each rank takes its block-aligned shard of one WAL, walks it independently
-(no data-path collective), and rank 0 stitches logical records across the
-shard boundary; the result must equal reading the whole file.  Also checks
-bench.py's Dist helper (barrier / max / sum over gloo)."""
+Each rank takes its block-aligned shard of one WAL and walks it through the
+C-ABI (revel_wal_shard_boundary_host: no GPU, no CRC -- a Reader with
+checksum == false), the ranks exchange only their boundary blobs, and rank 0
+stitches them (revel_wal_stitch_new); the logical-record view must equal
+reading the whole file.  Also checks bench.py's Dist helper (barrier / max /
+sum over gloo)."""
 import os
 import socket
 
@@ -28,15 +30,17 @@ def _worker(rank, world, port, image, q):
     import bench
     from revel_amd import shard
     D = bench.Dist()
-    s, e = shard.block_ranges(len(image), world)[rank]
-    recs = shard.physical_records(image[s:e], base_offset=s)
+    ranges = shard.block_ranges(len(image), world)
+    s, e = ranges[rank]
+    blob = shard.boundary_host(image, s, e - s)
     gathered = [None] * world
-    D.dist.all_gather_object(gathered, recs)
+    D.dist.all_gather_object(gathered, blob)
     D.barrier()
     mx = D.max(float(rank + 1))
     sm = D.sum(1.0)
     if rank == 0:
-        q.put((shard.stitch(gathered), mx, sm, [len(g) for g in gathered]))
+        st = shard.Stitch(gathered)
+        q.put((st.summary(), st.records(), ranges, mx, sm))
     D.close()
 
 
@@ -56,21 +60,13 @@ def test_sharded_walk_and_stitch_gloo(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, image, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got, mx, sm, counts = q.get(timeout=120)
+    summ, stitched, ranges, mx, sm = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert all(c > 0 for c in counts)
-    assert got == recs == po.read_all(image, checksum=False)
+    from test_shard import events_by_shards
+    assert recs == po.read_all(image, checksum=False)
+    assert events_by_shards(image, ranges, stitched) == recs
+    assert summ["records"] == len(recs) and summ["errors"] == 0 and summ["stitched"] >= 1
+    assert summ["payload_bytes"] == sum(len(r) for r in recs)
     assert mx == float(world) and sm == float(world)
-
-
-def test_block_ranges_cover_exactly():
-    from revel_amd import shard
-    for n in [0, 1, 32768, 32769, 10 * 32768 + 5]:
-        for w in [1, 2, 3, 8]:
-            rs = shard.block_ranges(n, w)
-            assert rs[0][0] == 0 and rs[-1][1] == n
-            for (a, b), (c, d) in zip(rs, rs[1:]):
-                assert b == c
-            assert all(a % 32768 == 0 or a == n for a, _ in rs)

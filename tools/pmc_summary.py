@@ -35,7 +35,10 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--json")
     ap.add_argument("--blocks", type=int, default=1 << 20)
-    ap.add_argument("--kernel", default="k_full_blocks<0, 1024, 1, false>")
+    ap.add_argument("--kernel", default="k_full_blocks4<1024, false>")
+    ap.add_argument("--library", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                       "revel_amd", "librevel_wal.so"),
+                    help="the librevel_wal.so the PMC pass ran (its SHA-256 goes into the json)")
     a = ap.parse_args()
     res = load(a.dir)
     for k, cs in res.items():
@@ -56,7 +59,10 @@ def main():
             raise SystemExit(f"kernel {a.kernel} not found; have {list(res)}")
         fetch = cs.get("FETCH_SIZE")
         write = cs.get("WRITE_SIZE")
-        out = {"kernel": a.kernel, "blocks": a.blocks,
+        import hashlib
+        with open(a.library, "rb") as fh:
+            sha = hashlib.sha256(fh.read()).hexdigest()
+        out = {"kernel": a.kernel, "blocks": a.blocks, "library_sha256": sha,
                "fetch_size_kib": fetch, "write_size_kib": write,
                "hbm_read_bytes_per_launch": None if fetch is None else 2 * fetch * 1024,
                "hbm_write_bytes_per_launch": None if write is None else write * 1024,
