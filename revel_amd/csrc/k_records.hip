@@ -1110,7 +1110,7 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
 // k_verify_rows; !ROWS = v3 over those blocks (experiments only, with its
 // TQ / R64 / TQ8 load shapes).  Lists: verify = hlist + overflow entries in the
 // result slots (xlist = out, 3 u64 apart); FRAME = framing list.
-template <bool FRAME, bool ROWS = true, bool TQ = false, bool R64 = false, bool TQ8 = false>
+template <bool FRAME, bool ROWS = true, bool TQ = false, bool R64 = false, bool TQ8 = false, int ROWS_RING = kRowsRing>
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
@@ -1123,12 +1123,13 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
             hipError_t e = hipMemsetAsync(d_blist, 0, 4, st);
             if (e != hipSuccess) return e;
             const uint64_t nb = b_hi - b_lo;
+            const uint64_t per_wg = kSparseThreads * kSparsePer;
             hipLaunchKernelGGL(k_sparse_blocks,
-                               dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu * 4, (nb + 255) / 256))),
-                               dim3(256), 0, st, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist + 1, d_blist);
+                               dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nb + per_wg - 1) / per_wg))),
+                               dim3(kSparseThreads), 0, st, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist + 1, d_blist);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((k_verify_rows<FRAME, kRowsRing>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
+            hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + 1, d_blist);
         } else {
             const uint64_t waves = kVerify2Threads / 64;

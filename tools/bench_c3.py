@@ -89,6 +89,9 @@ def main():
             e1.record()
             if variant == 0:  # production, from the product library
                 check(L.revel_gpu_verify_records(ctx.handle, d.ptr, n, 0, first.ptr, out.ptr, None))
+            elif variant >= 100:  # a production-library verify path (test hook), variant - 100
+                check(L.revel_gpu_verify_records_path(ctx.handle, variant - 100, d.ptr, n, 0, first.ptr, out.ptr,
+                                                      None))
             else:  # experiment arms (tools/experiments/libexperiments.so)
                 check(experiments().revel_x_verify_records_variant(ctx.handle, variant, d.ptr, n, 0, first.ptr,
                                                                    out.ptr, None))

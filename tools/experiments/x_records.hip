@@ -36,6 +36,30 @@ uint32_t grid_for(const DeviceInfo& di, uint64_t n, uint64_t waves) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + waves - 1) / waves));
 }
 
+// k_verify_rows with another ring depth / workgroup size (production: 8 rows, 1024 threads)
+template <int RING, int THREADS>
+hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
+                             const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
+                             const uint32_t* d_counts, const uint64_t* xl, uint32_t xs, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t b_hi = nbytes / kBlockSize;
+    uint32_t* d_blist = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(hl) + nblocks * kListStride);
+    if (b_hi) {
+        hipError_t e = hipMemsetAsync(d_blist, 0, 4, st);
+        if (e != hipSuccess) return e;
+        const uint64_t per_wg = kSparseThreads * kSparsePer;
+        hipLaunchKernelGGL(k_sparse_blocks,
+                           dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (b_hi + per_wg - 1) / per_wg))),
+                           dim3(kSparseThreads), 0, st, d_counts, 0u, (uint32_t)b_hi, d_blist + 1, d_blist);
+        hipLaunchKernelGGL((k_verify_rows<false, RING, THREADS>), dim3((uint32_t)std::max(1, di.num_cu)),
+                           dim3(THREADS), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl, d_blist + 1,
+                           d_blist);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl, xs, st);
+}
+
 hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                     const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                     const uint32_t* d_counts, hipStream_t st) {
@@ -101,6 +125,21 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
             if (!lists) return hipErrorInvalidValue;
             return launch_verify_split<false, false, true, false, true>(di, img, nbytes, base_offset, d_first, d_out,
                                                                         0u, hl, d_counts, xl, xs, st);
+        case 20:  // rows, 16-row ring, 768 threads
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 768>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 21:  // rows, 16-row ring, 512 threads
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 512>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 22:  // rows, 8-row ring, 768 threads
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 768>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 23:  // rows, 16-row ring, 1024 threads
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 1024>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 24:  // production shape through this module (control for 20-23)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
         case 15:  // session-5 production: v3 over the sparse whole blocks
             if (!lists) return hipErrorInvalidValue;
             return launch_verify_split<false, false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
