@@ -151,7 +151,8 @@ int revel_gpu_context_new(int device, revel_gpu_context** out);
  * after this call). */
 void revel_gpu_context_free(revel_gpu_context* ctx);
 /* Drop the window buffers a freed reader parked on the context for the next
- * reader (pinned + device memory of about twice its window). */
+ * reader (pinned + device memory of about twice its window) and the pinned
+ * ring a shard load keeps for the next one (3 windows). */
 int revel_gpu_context_trim(revel_gpu_context* ctx);
 /* The context's stream as an opaque hipStream_t. */
 void* revel_gpu_context_stream(revel_gpu_context* ctx);
@@ -413,7 +414,10 @@ typedef struct revel_wal_shard_info {
     const revel_record_result* d_phys;
     const revel_logical_record* d_events;  /* READ */
     const void* d_payload;       /* READ */
-    double seconds;              /* host wall time of the load (read + H2D + verify [+ reassembly]) */
+    double setup_seconds;        /* allocating the shard's HBM buffers (+ the pinned ring, first load
+                                    on a context only: the ring is kept on the context) */
+    double seconds;              /* host wall time of the pipeline after setup: read + H2D + verify
+                                    [+ reassembly] + boundary */
     double read_seconds;         /* summed host time filling pinned windows */
     double h2d_ms, kernel_ms;    /* summed H2D time / verify (+ reassembly) time, HIP events */
 } revel_wal_shard_info;

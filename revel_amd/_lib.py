@@ -50,7 +50,8 @@ class ShardInfo(Structure):
     _fields_ = [("device", c_int), ("checksum", c_int), ("offset", c_uint64), ("length", c_uint64),
                 ("file_bytes", c_uint64), ("physical", c_uint64), ("bad", c_uint64), ("events", c_uint64),
                 ("records", c_uint64), ("payload_bytes", c_uint64), ("d_image", c_void_p), ("d_phys", c_void_p),
-                ("d_events", c_void_p), ("d_payload", c_void_p), ("seconds", ctypes.c_double),
+                ("d_events", c_void_p), ("d_payload", c_void_p), ("setup_seconds", ctypes.c_double),
+                ("seconds", ctypes.c_double),
                 ("read_seconds", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double)]
 
     def as_dict(self):

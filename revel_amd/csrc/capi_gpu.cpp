@@ -33,8 +33,21 @@ using revel::set_error;
 
 namespace revel {
 
+void free_shard_ring(revel_gpu_context* ctx) {
+    auto& R = ctx->shard_ring;
+    if (R.copy) (void)hipStreamSynchronize(R.copy);
+    for (int i = 0; i < revel_gpu_context::ShardRing::kSlots; ++i) {
+        if (R.h[i]) (void)hipHostFree(R.h[i]);
+        if (R.e0[i]) (void)hipEventDestroy(R.e0[i]);
+        if (R.e1[i]) (void)hipEventDestroy(R.e1[i]);
+    }
+    if (R.copy) (void)hipStreamDestroy(R.copy);
+    R = revel_gpu_context::ShardRing{};
+}
+
 void destroy_context(revel_gpu_context* ctx) {
     DeviceGuard guard(ctx->di.device);
+    free_shard_ring(ctx);
     if (ctx->stream) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamDestroy(ctx->stream);
@@ -193,6 +206,7 @@ int revel_gpu_context_trim(revel_gpu_context* ctx) {
     if (pr.d_first) HIP_TRY(hipFree(pr.d_first), "hipFree");
     if (pr.d_out) HIP_TRY(hipFree(pr.d_out), "hipFree");
     pr = revel_gpu_context::ParkedReader{};
+    revel::free_shard_ring(ctx);
     return REVEL_OK;
 }
 

@@ -189,6 +189,8 @@ class DeviceGuard {
     hipError_t err_ = hipSuccess;
 };
 
+// Frees the context's cached shard-load ring (device bound by the caller).
+void free_shard_ring(revel_gpu_context* ctx);
 // Releases the context's resources now (no readers left).  Internal: the
 // public revel_gpu_context_free defers to the last reader.
 void destroy_context(revel_gpu_context* ctx);
@@ -230,6 +232,16 @@ struct revel_gpu_context {
         revel_record_result* d_out = nullptr;
         size_t d_out_cap = 0;
     } parked_reader;
+    // Pinned load ring (windows + copy stream + events) of the last
+    // revel_gpu_wal_shard_load on this context, kept for the next load with
+    // the same window; freed with the context or by revel_gpu_context_trim.
+    struct ShardRing {
+        static constexpr int kSlots = 3;
+        size_t window = 0;
+        hipStream_t copy = nullptr;
+        uint8_t* h[kSlots] = {};
+        hipEvent_t e0[kSlots] = {}, e1[kSlots] = {};
+    } shard_ring;
     // Lifetime: live readers pin the context; revel_gpu_context_free with
     // readers still alive only marks it, and the last reader's release
     // destroys it (revel_wal.h, "GPU context").

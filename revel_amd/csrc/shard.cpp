@@ -110,20 +110,29 @@ struct revel_wal_shard {
 
 namespace {
 
-// Pinned windows + copy stream of one shard load.
-struct LoadRing {
-    hipStream_t copy = nullptr;
-    std::vector<uint8_t*> h;
-    std::vector<hipEvent_t> e0, e1;
-    std::vector<bool> used;
-    ~LoadRing() {
-        for (size_t i = 0; i < h.size(); ++i) {
-            if (used[i]) (void)hipEventSynchronize(e1[i]);
-            if (h[i]) (void)hipHostFree(h[i]);
-            if (e0[i]) (void)hipEventDestroy(e0[i]);
-            if (e1[i]) (void)hipEventDestroy(e1[i]);
-        }
-        if (copy) (void)hipStreamDestroy(copy);
+// The context's cached pinned ring for a load with `window`-byte windows:
+// (re)allocated when the window size changes; every slot's pending H2D is
+// waited for when the load ends, successful or not.
+int ring_for(revel_gpu_context* ctx, size_t window) {
+    auto& R = ctx->shard_ring;
+    if (R.copy && R.window == window) return REVEL_OK;
+    revel::free_shard_ring(ctx);
+    TRY(hipStreamCreateWithFlags(&R.copy, hipStreamNonBlocking), "hipStreamCreate(copy)");
+    for (int i = 0; i < revel_gpu_context::ShardRing::kSlots; ++i) {
+        TRY(hipHostMalloc(reinterpret_cast<void**>(&R.h[i]), window, hipHostMallocDefault), "hipHostMalloc(window)");
+        TRY(hipEventCreate(&R.e0[i]), "hipEventCreate");
+        TRY(hipEventCreate(&R.e1[i]), "hipEventCreate");
+    }
+    R.window = window;
+    return REVEL_OK;
+}
+
+struct RingDrain {
+    revel_gpu_context::ShardRing& R;
+    bool used[revel_gpu_context::ShardRing::kSlots] = {};
+    ~RingDrain() {
+        for (int i = 0; i < revel_gpu_context::ShardRing::kSlots; ++i)
+            if (used[i]) (void)hipEventSynchronize(R.e1[i]);
     }
 };
 
@@ -271,24 +280,19 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
         size_t w = window_bytes ? window_bytes : (64u << 20);
         w = (w + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE * REVEL_BLOCK_SIZE;
         w = (size_t)std::min<uint64_t>(w, nblocks * REVEL_BLOCK_SIZE);
-        const int nbuf = 3;
-        LoadRing R;
-        TRY(hipStreamCreateWithFlags(&R.copy, hipStreamNonBlocking), "hipStreamCreate(copy)");
-        R.h.assign(nbuf, nullptr);
-        R.e0.assign(nbuf, nullptr);
-        R.e1.assign(nbuf, nullptr);
-        R.used.assign(nbuf, false);
-        for (int i = 0; i < nbuf; ++i) {
-            TRY(hipHostMalloc(reinterpret_cast<void**>(&R.h[i]), w, hipHostMallocDefault), "hipHostMalloc(window)");
-            TRY(hipEventCreate(&R.e0[i]), "hipEventCreate");
-            TRY(hipEventCreate(&R.e1[i]), "hipEventCreate");
-        }
+        constexpr int nbuf = revel_gpu_context::ShardRing::kSlots;
+        int rc0 = ring_for(ctx, w);
+        if (rc0) return rc0;
+        auto& R = ctx->shard_ring;
+        RingDrain drain{R};
+        const auto t_pipe = std::chrono::steady_clock::now();
+        I.setup_seconds = std::chrono::duration<double>(t_pipe - t0).count();
         auto retire = [&](int slot) -> int {
             TRY(hipEventSynchronize(R.e1[slot]), "hipEventSynchronize(H2D)");
             float ms = 0;
             TRY(hipEventElapsedTime(&ms, R.e0[slot], R.e1[slot]), "hipEventElapsedTime");
             I.h2d_ms += ms;
-            R.used[slot] = false;
+            drain.used[slot] = false;
             return REVEL_OK;
         };
         const int threads = std::max(1, io_threads);
@@ -296,7 +300,7 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
         for (uint64_t i = 0; off < length; ++i) {
             const int slot = (int)(i % nbuf);
             int rc;
-            if (R.used[slot] && (rc = retire(slot))) return rc;
+            if (drain.used[slot] && (rc = retire(slot))) return rc;
             const uint64_t len = std::min<uint64_t>(w, length - off);
             uint8_t* h = R.h[slot];
             I.read_seconds += revel::parallel_fill(threads, len, [&](uint64_t o, uint64_t n) {
@@ -306,7 +310,7 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
             TRY(hipMemcpyAsync(static_cast<uint8_t*>(s->d_image) + off, h, len, hipMemcpyHostToDevice, R.copy),
                 "hipMemcpyAsync(H2D)");
             TRY(hipEventRecord(R.e1[slot], R.copy), "hipEventRecord");
-            R.used[slot] = true;
+            drain.used[slot] = true;
             TRY(hipStreamWaitEvent(comp, R.e1[slot], 0), "hipStreamWaitEvent");
             const uint64_t b0 = off / REVEL_BLOCK_SIZE;
             TRY(revel::count_records(ctx->di, static_cast<uint8_t*>(s->d_image) + off, len, s->d_counts + b0,
@@ -316,7 +320,7 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
         }
         for (int slot = 0; slot < nbuf; ++slot) {
             int rc;
-            if (R.used[slot] && (rc = retire(slot))) return rc;
+            if (drain.used[slot] && (rc = retire(slot))) return rc;
         }
         hipEvent_t k0 = nullptr, k1 = nullptr;
         TRY(hipEventCreate(&k0), "hipEventCreate");
@@ -383,7 +387,7 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
     H.records = I.records;
     H.payload_bytes = I.payload_bytes;
     H.checksum = I.checksum;
-    I.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    I.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() - I.setup_seconds;
     return REVEL_OK;
 }
 
