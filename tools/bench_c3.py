@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=1 << 30, help="size of the written Zipf image")
     ap.add_argument("--tile", type=int, default=4, help="repeat the image's whole blocks this many times")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds over the variants")
     ap.add_argument("--variants", default="0,15")
     ap.add_argument("--image", choices=["zipf", "full"], default="zipf",
                     help="full = C2-style full blocks (1 record/block): the verify kernels' base cost")
@@ -80,27 +81,40 @@ def main():
     out = ctx.alloc(nrec * 24)
     L = lib()
     e0, e1, e2 = ctx.event(), ctx.event(), ctx.event()
-    for variant in [int(v) for v in a.variants.split(",")]:
-        times_all, times_verify = [], []
-        for _ in range(a.iters):
-            e0.record()
-            check(L.revel_gpu_count_records(ctx.handle, d.ptr, n, counts.ptr, None))
-            check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
-            e1.record()
-            if variant == 0:  # production, from the product library
-                check(L.revel_gpu_verify_records(ctx.handle, d.ptr, n, 0, first.ptr, out.ptr, None))
-            elif variant >= 100:  # a production-library verify path (test hook), variant - 100
-                check(L.revel_gpu_verify_records_path(ctx.handle, variant - 100, d.ptr, n, 0, first.ptr, out.ptr,
-                                                      None))
-            else:  # experiment arms (tools/experiments/libexperiments.so)
-                check(experiments().revel_x_verify_records_variant(ctx.handle, variant, d.ptr, n, 0, first.ptr,
-                                                                   out.ptr, None))
-            e2.record()
-            ctx.sync()
-            times_all.append(e0.elapsed_ms(e2))
-            times_verify.append(e1.elapsed_ms(e2))
-        got = ctx.d2h(out, nrec * 24, np.uint8).view(res.dtype)
-        same = bool(np.array_equal(got, res))
+    variants = [int(v) for v in a.variants.split(",")]
+
+    def run(variant):
+        e0.record()
+        check(L.revel_gpu_count_records(ctx.handle, d.ptr, n, counts.ptr, None))
+        check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+        e1.record()
+        if variant == 0:  # production, from the product library
+            check(L.revel_gpu_verify_records(ctx.handle, d.ptr, n, 0, first.ptr, out.ptr, None))
+        elif variant >= 100:  # a production-library verify path (test hook), variant - 100
+            check(L.revel_gpu_verify_records_path(ctx.handle, variant - 100, d.ptr, n, 0, first.ptr, out.ptr,
+                                                  None))
+        else:  # experiment arms (tools/experiments/libexperiments.so)
+            check(experiments().revel_x_verify_records_variant(ctx.handle, variant, d.ptr, n, 0, first.ptr,
+                                                               out.ptr, None))
+        e2.record()
+        ctx.sync()
+        return e0.elapsed_ms(e2), e1.elapsed_ms(e2)
+
+    # interleaved rounds (--rounds > 1): every variant once per round, so drift
+    # (clock, temperature) spreads over all of them; medians per variant
+    times = {v: ([], []) for v in variants}
+    same_all = {v: True for v in variants}
+    for _ in range(max(1, a.rounds)):
+        for variant in variants:
+            for _ in range(a.iters):
+                ta, tv = run(variant)
+                times[variant][0].append(ta)
+                times[variant][1].append(tv)
+            got = ctx.d2h(out, nrec * 24, np.uint8).view(res.dtype)
+            same_all[variant] = same_all[variant] and bool(np.array_equal(got, res))
+    for variant in variants:
+        times_all, times_verify = times[variant]
+        same = same_all[variant]
         ta, tv = float(np.median(times_all)), float(np.median(times_verify))
         print(json.dumps({
             "workload": ("C3 zipf 64B-32KiB records (1 GiB written by the host writer, whole blocks tiled), device walk + segmented CRC verify"
