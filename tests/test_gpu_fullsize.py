@@ -1,0 +1,158 @@
+"""GPU parity at BASELINE.json's full sizes, through size-independent
+properties (the oracle checks every value where it can in seconds):
+
+* C2: 1 M blocks = 32 GiB synthesised + framed on the device, every masked
+  CRC checked against the C oracle (SSE4.2 restatement, cross-checked with the
+  bytewise one on a sample) over the whole 32 GiB, then 257 blocks corrupted
+  -> exactly those flagged;
+* C3: a 1 GiB Zipf image framed on the device (revel_gpu_append_records),
+  verified: every record OK, record count = the host fragment layout,
+  computed == stored; 1 000 payload bit flips -> exactly those records flagged;
+* one WAL across 3 contexts at 256 MiB: the sharded replay's stream equals the
+  oracle Reader's, and its counts equal the whole-image verify's."""
+import numpy as np
+import pytest
+
+from revel_amd import BLOCK_SIZE, shard
+from revel_amd._lib import RevelError
+from oracle import crc32c_oracle as po
+from oracle import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+
+
+def test_c2_full_size_every_crc_vs_oracle(gpu_ctx):
+    n = 1 << 20
+    d = gpu_ctx.alloc(n * BLOCK_SIZE)
+    gpu_ctx.synth_full_blocks(d, n, seed=0x5EED0002)
+    m, ok = gpu_ctx.alloc(4 * n), gpu_ctx.alloc(n)
+    gpu_ctx.crc_full_blocks(d, n, m, ok)
+    gpu_ctx.sync()
+    got = gpu_ctx.d2h(m, 4 * n, np.uint32)
+    assert gpu_ctx.d2h(ok, n).all()
+    chunk = 32768  # 1 GiB of blocks per host pass
+    for b0 in range(0, n, chunk):
+        host = gpu_ctx.d2h(d, chunk * BLOCK_SIZE, src_offset=b0 * BLOCK_SIZE).reshape(chunk, BLOCK_SIZE)
+        want = oc.full_block_crcs(host, "sse42")
+        assert np.array_equal(got[b0:b0 + chunk], want), b0
+        if b0 == 0:
+            assert np.array_equal(want[:256], oc.full_block_crcs(host[:256], "bytewise"))
+        # the stored header is what the writer would have stored
+        assert np.array_equal(host[:, 0:4].copy().view(np.uint32).ravel(), want)
+    rng = np.random.default_rng(2)
+    bad = np.sort(rng.choice(n, 257, replace=False))
+    for b in bad:
+        pos = int(rng.integers(6, BLOCK_SIZE))
+        byte = gpu_ctx.d2h(d, 1, src_offset=int(b) * BLOCK_SIZE + pos)
+        gpu_ctx.h2d(d, byte ^ np.uint8(1 << int(rng.integers(0, 8))), dst_offset=int(b) * BLOCK_SIZE + pos)
+    gpu_ctx.crc_full_blocks(d, n, m, ok)
+    gpu_ctx.sync()
+    assert np.array_equal(np.flatnonzero(gpu_ctx.d2h(ok, n) == 0), bad)
+
+
+def test_c3_full_size_append_verify_roundtrip(gpu_ctx):
+    rng = np.random.default_rng(0x5EED0003)
+    k = np.arange(1, 513)
+    p = k ** -1.1
+    p /= p.sum()
+    target = 1 << 30
+    sizes = (64 * rng.choice(k, size=target // 3000 + 4096, p=p)).astype(np.uint64)
+    sizes = sizes[:int(np.searchsorted(np.cumsum(sizes + 7), target))]
+    nb_pay = (int(sizes.sum()) + BLOCK_SIZE - 1) // BLOCK_SIZE
+    pay = gpu_ctx.alloc(nb_pay * BLOCK_SIZE)
+    gpu_ctx.synth_full_blocks(pay, nb_pay, seed=0x5EED0003)
+    img, n, bo = gpu_ctx.append_records(pay, sizes)
+    # the host layout (log_writer.rs:58-97) predicts the image size and the fragment count
+    assert n == po_framed_size(sizes)
+    nfrag = po_fragment_count(sizes)
+    res = gpu_ctx.verify_image(img, n)
+    assert len(res) == nfrag
+    assert (res["status"] == 0).all()
+    assert np.array_equal(res["computed_crc"], res["stored_crc"])
+    assert int(res["length"].astype(np.uint64).sum()) == int(sizes.sum())
+    # 1 000 payload bit flips -> exactly those records flagged
+    cand = np.flatnonzero(res["length"] > 0)
+    victims = np.sort(rng.choice(cand, 1000, replace=False))
+    for v in victims:
+        off = int(res["file_offset"][v]) + 7 + int(rng.integers(0, int(res["length"][v])))
+        byte = gpu_ctx.d2h(img, 1, src_offset=off)
+        gpu_ctx.h2d(img, byte ^ np.uint8(0x20), dst_offset=off)
+    res2 = gpu_ctx.verify_image(img, n)
+    assert np.array_equal(np.flatnonzero(res2["status"] != 0), victims)
+    assert (res2["status"][victims] == 1).all()
+
+
+def po_framed_size(sizes):
+    import revel_amd
+    return revel_amd.lib().revel_log_framed_size(np.ascontiguousarray(sizes, dtype=np.uint64).ctypes.data,
+                                                 len(sizes), 0)
+
+
+def po_fragment_count(sizes):
+    """Physical records n successive add_record calls emit (log_writer.rs:58-97)."""
+    boff, count = 0, 0
+    for s in sizes.tolist():
+        left, begin = s, True
+        while True:
+            if BLOCK_SIZE - boff < 7:
+                boff = 0
+            avail = BLOCK_SIZE - boff - 7
+            frag = min(left, avail)
+            count += 1
+            boff += 7 + frag
+            left -= frag
+            if left == 0:
+                break
+    return count
+
+
+def test_sharded_replay_256mib_three_contexts():
+    from revel_amd import gpu as G
+    rng = np.random.default_rng(77)
+    k = np.arange(1, 513)
+    p = k ** -1.1
+    p /= p.sum()
+    sizes = 64 * rng.choice(k, size=70000, p=p)
+    blob = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8).tobytes()
+    recs, off = [], 0
+    for s in sizes:
+        recs.append(blob[off:off + int(s)])
+        off += int(s)
+    img = bytearray(oc.write_image(recs))
+    ref = oc.walk(bytes(img))
+    for v in rng.choice(np.flatnonzero(ref["length"] > 0), 50, replace=False):
+        img[int(ref["file_offset"][v]) + 7] ^= 1
+    img = bytes(img)
+    ctxs = [G.GpuContext(0) for _ in range(3)]
+    try:
+        r = shard.ShardedReplay(ctxs, image=img, checksum=True, window_bytes=8 << 20)
+        got = []
+        errors = 0
+        while True:
+            try:
+                x = r.read_record()
+            except RevelError:
+                errors += 1
+                continue
+            if x is None:
+                break
+            got.append(x)
+        rd = po.LogReader(img, True)
+        want, werr = [], 0
+        while True:
+            try:
+                x = rd.read_record()
+            except po.CorruptionError:
+                werr += 1
+                continue
+            if x is None:
+                break
+            want.append(x)
+        assert got == want and errors == werr == 50
+        s = r.summary()
+        assert s["physical"] == len(ref) and s["bad"] == 50 and s["records"] == len(want)
+        assert s["stitched"] >= 1
+        r.close()
+    finally:
+        for c in ctxs:
+            c.close()
