@@ -37,7 +37,7 @@ uint32_t grid_for(const DeviceInfo& di, uint64_t n, uint64_t waves) {
 }
 
 // k_verify_rows with another ring depth / workgroup size (production: 8 rows, 1024 threads)
-template <int RING, int THREADS, int DIAG = 0>
+template <int RING, int THREADS, int DIAG = 0, int NB = 4>
 hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                              const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
                              const uint32_t* d_counts, const uint64_t* xl, uint32_t xs, hipStream_t st) {
@@ -51,7 +51,7 @@ hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t 
         hipLaunchKernelGGL(k_sparse_blocks,
                            dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (b_hi + per_wg - 1) / per_wg))),
                            dim3(kSparseThreads), 0, st, d_counts, 0u, (uint32_t)b_hi, d_blist + 1, d_blist);
-        hipLaunchKernelGGL((k_verify_rows<false, RING, THREADS, DIAG>), dim3((uint32_t)std::max(1, di.num_cu)),
+        hipLaunchKernelGGL((k_verify_rows<false, RING, THREADS, DIAG, NB>), dim3((uint32_t)std::max(1, di.num_cu)),
                            dim3(THREADS), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl, d_blist + 1,
                            d_blist);
         e = hipGetLastError();
@@ -155,6 +155,9 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
             if (variant == 26)
                 return launch_rows_shape<8, 1024, 2>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
             return launch_rows_shape<8, 1024, 3>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 30:  // rows with eight captures per flush
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 0, 8>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
         case 15:  // session-5 production: v3 over the sparse whole blocks
             if (!lists) return hipErrorInvalidValue;
             return launch_verify_split<false, false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts,
