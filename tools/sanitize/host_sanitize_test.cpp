@@ -2,14 +2,16 @@
 // AddressSanitizer + UndefinedBehaviorSanitizer (host code only; no GPU
 // sanitizer exists on this pool).  Exercises every host-side C-ABI path:
 // CRC, memory/posix files, the writer, the checksum=0 reader (host walk),
-// initial_offset, framed-size layout, corruption and the error returns of
-// the GPU entry points without a device.  Built by tools/sanitize/Makefile;
+// initial_offset, framed-size layout, corruption, caller-implemented files
+// (callbacks, short reads, release), the shard boundary walk + stitch, and
+// the error returns of the GPU entry points without a device.  Built by tools/sanitize/Makefile;
 // run by tests/test_sanitize.py.  Exit 0 = all checks passed, no reports.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <random>
 #include <string>
 #include <vector>
@@ -57,6 +59,37 @@ static std::vector<Bytes> read_all(const Bytes& img, uint64_t initial_offset, si
     revel_log_reader_free(r);
     return out;
 }
+
+// A caller's files behind the callback adapters (env.rs:40-57).
+struct VecW {
+    Bytes b;
+    int flushes = 0, syncs = 0, closes = 0, released = 0;
+    size_t fail_after = (size_t)-1;
+};
+static int vw_append(void* u, const uint8_t* d, size_t n) {
+    auto* f = static_cast<VecW*>(u);
+    if (f->b.size() + n > f->fail_after) return REVEL_IO_ERROR;
+    f->b.insert(f->b.end(), d, d + n);
+    return REVEL_OK;
+}
+static int vw_flush(void* u) { return ++static_cast<VecW*>(u)->flushes, REVEL_OK; }
+static int vw_sync(void* u) { return ++static_cast<VecW*>(u)->syncs, REVEL_OK; }
+static int vw_close(void* u) { return ++static_cast<VecW*>(u)->closes, 99; }  // out-of-range code -> IOError
+static void vw_release(void* u) { ++static_cast<VecW*>(u)->released; }
+struct VecR {
+    const Bytes* b;
+    size_t pos = 0, chunk = 1;
+    int released = 0;
+};
+static int vr_read(void* u, uint8_t* p, size_t n, size_t* got) {
+    auto* r = static_cast<VecR*>(u);
+    size_t k = std::min(std::min(n, r->chunk), r->b->size() - std::min(r->pos, r->b->size()));
+    if (k) memcpy(p, r->b->data() + r->pos, k);
+    r->pos += k;
+    *got = k;
+    return REVEL_OK;
+}
+static void vr_release(void* u) { ++static_cast<VecR*>(u)->released; }
 
 int main() {
     // ---- CRC known answers (crc.rs:50-76, RFC 3720 B.4) ----
@@ -152,6 +185,106 @@ int main() {
     CHECK(revel_sequential_file_read(ms, sc, 16, &got) == REVEL_OK && got == 5 && memcmp(sc, "56789", 5) == 0);
     CHECK(revel_sequential_file_read(ms, sc, 16, &got) == REVEL_OK && got == 0);
     revel_sequential_file_free(ms);
+
+    // ---- caller-implemented files ----
+    {
+        std::vector<Bytes> recs;
+        for (int i = 0; i < 40; ++i) {
+            Bytes r(rng() % 90000);
+            for (auto& b : r) b = (uint8_t)rng();
+            recs.push_back(r);
+        }
+        const Bytes want = write_image(recs, 0);
+        VecW vw;
+        revel_writable_file* cf = nullptr;
+        CHECK(revel_writable_file_from_callbacks(&vw, vw_append, vw_flush, vw_close, vw_sync, vw_release, &cf) ==
+              REVEL_OK);
+        revel_log_writer* cw = revel_log_writer_new(cf, 0);
+        for (const Bytes& r : recs) CHECK(revel_log_writer_add_record(cw, r.data(), r.size()) == REVEL_OK);
+        CHECK(revel_writable_file_sync(cf) == REVEL_OK && vw.syncs == 1);
+        CHECK(revel_writable_file_close(cf) == REVEL_IO_ERROR && vw.closes == 1);
+        CHECK(vw.b == want && vw.flushes >= 40);
+        revel_log_writer_free(cw);
+        revel_writable_file_free(cf);
+        CHECK(vw.released == 1);
+        VecW full;
+        full.fail_after = 1000;
+        revel_writable_file* ff = nullptr;
+        CHECK(revel_writable_file_from_callbacks(&full, vw_append, nullptr, nullptr, nullptr, nullptr, &ff) == REVEL_OK);
+        revel_log_writer* fw = revel_log_writer_new(ff, 0);
+        Bytes big2(5000, 1);
+        CHECK(revel_log_writer_add_record(fw, big2.data(), big2.size()) == REVEL_IO_ERROR);
+        revel_log_writer_free(fw);
+        revel_writable_file_free(ff);
+        CHECK(revel_writable_file_from_callbacks(&vw, nullptr, nullptr, nullptr, nullptr, nullptr, &ff) ==
+              REVEL_INVALID_ARGUMENT);
+        for (size_t chunk : {(size_t)1, (size_t)7, (size_t)4096, (size_t)1 << 30}) {
+            VecR vr{&want, 0, chunk};
+            revel_sequential_file* sf = nullptr;
+            CHECK(revel_sequential_file_from_callbacks(&vr, vr_read, nullptr, vr_release, &sf) == REVEL_OK);
+            revel_log_reader* cr = nullptr;
+            CHECK(revel_log_reader_new(sf, 0, chunk == 7 ? 40000 : 0, nullptr, 65536, &cr) == REVEL_OK);
+            size_t k = 0;
+            for (;;) {
+                const uint8_t* dd = nullptr;
+                size_t nn = 0;
+                if (revel_log_reader_read_record(cr, &dd, &nn) != REVEL_OK) continue;
+                if (!dd) break;
+                if (chunk != 7) CHECK(k < recs.size() && Bytes(dd, dd + nn) == recs[k]);
+                ++k;
+            }
+            if (chunk != 7) CHECK(k == recs.size());
+            revel_log_reader_free(cr);
+            CHECK(vr.released == 1);
+        }
+    }
+
+    // ---- shard boundaries + stitch (host walk) ----
+    {
+        std::vector<Bytes> recs;
+        for (int i = 0; i < 50; ++i) {
+            Bytes r(rng() % 150000);
+            for (auto& b : r) b = (uint8_t)rng();
+            recs.push_back(r);
+        }
+        Bytes img = write_image(recs, 0);
+        img[img.size() / 3] ^= 0x11;  // some corruption (a header byte or payload)
+        for (int nsh : {1, 2, 3, 7, 16}) {
+            std::vector<uint64_t> offs(nsh + 1);
+            CHECK(revel_wal_shard_ranges(img.size(), nsh, offs.data()) == REVEL_OK);
+            std::vector<Bytes> blobs(nsh);
+            std::vector<const uint8_t*> ptrs(nsh);
+            std::vector<size_t> sizes(nsh);
+            for (int k = 0; k < nsh; ++k) {
+                size_t need = 0;
+                CHECK(revel_wal_shard_boundary_host(img.data(), img.size(), offs[k], offs[k + 1] - offs[k],
+                                                    REVEL_SHARD_READ, nullptr, 0, &need) == REVEL_OK);
+                blobs[k].resize(need);
+                CHECK(revel_wal_shard_boundary_host(img.data(), img.size(), offs[k], offs[k + 1] - offs[k],
+                                                    REVEL_SHARD_READ, blobs[k].data(), need, &need) == REVEL_OK);
+                ptrs[k] = blobs[k].data();
+                sizes[k] = blobs[k].size();
+            }
+            revel_wal_stitch* st = nullptr;
+            CHECK(revel_wal_stitch_new(ptrs.data(), sizes.data(), nsh, &st) == REVEL_OK);
+            revel_wal_summary sum;
+            CHECK(revel_wal_stitch_summary(st, &sum) == REVEL_OK);
+            CHECK(sum.bytes == img.size());
+            for (size_t i = 0; i < sum.stitched; ++i) {
+                uint64_t fo = 0, nn = 0;
+                const uint8_t* dd = nullptr;
+                int before = -1;
+                CHECK(revel_wal_stitch_record(st, i, &fo, &dd, &nn, &before) == REVEL_OK);
+                CHECK(before > 0 && before < nsh && (dd != nullptr || nn == 0));
+            }
+            revel_wal_stitch_free(st);
+            // truncated blobs are rejected, not read past
+            if (nsh > 1) {
+                sizes[1] -= 1;
+                CHECK(revel_wal_stitch_new(ptrs.data(), sizes.data(), nsh, &st) == REVEL_INVALID_ARGUMENT);
+            }
+        }
+    }
 
     // ---- GPU entry points fail loudly without a device; null arguments ----
     int count = -1;
