@@ -84,12 +84,32 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
     uint32_t p = 0;
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-        uint32_t am = (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - k, 1);
-        p ^= b & am;
-        uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
-        b = (b >> 1) ^ (kPolyReflected & bm);
+        p = __builtin_amdgcn_bitop3_b32(p, b, (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - k, 1), 0x78);
+        if (k < 31) {
+            const uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
+            b = __builtin_amdgcn_bitop3_b32(b >> 1, bm, kPolyReflected, 0x78);  // s0 ^ (s1 & s2)
+        }
     }
     return p;
+}
+
+// p1 = a1*b, p2 = a2*b: one shared chain b*x^k, two masked accumulations
+// 7 VALU per bit for both products: three v_bitop3 (0x78 = s0 ^ (s1 & s2)),
+// three v_bfe, one shift.  The builtins keep the compiler from re-associating
+// the chain into a longer form.
+__device__ __forceinline__ void gf_mul2(uint32_t b, uint32_t a1, uint32_t a2, uint32_t& p1, uint32_t& p2) {
+    uint32_t q1 = 0, q2 = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        q1 = __builtin_amdgcn_bitop3_b32(q1, b, (uint32_t)__builtin_amdgcn_sbfe((int)a1, 31 - k, 1), 0x78);
+        q2 = __builtin_amdgcn_bitop3_b32(q2, b, (uint32_t)__builtin_amdgcn_sbfe((int)a2, 31 - k, 1), 0x78);
+        if (k < 31) {
+            const uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
+            b = __builtin_amdgcn_bitop3_b32(b >> 1, bm, kPolyReflected, 0x78);
+        }
+    }
+    p1 = q1;
+    p2 = q2;
 }
 
 // x^(8n) mod P for 0 <= n <= 32768 from the two shift tables.

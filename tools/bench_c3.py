@@ -53,9 +53,14 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds over the variants")
     ap.add_argument("--variants", default="0,15")
+    ap.add_argument("--lib", default=None,
+                    help="load this build of librevel_wal.so instead of the in-tree one (A/B of two builds)")
     ap.add_argument("--image", choices=["zipf", "full"], default="zipf",
                     help="full = C2-style full blocks (1 record/block): the verify kernels' base cost")
     a = ap.parse_args()
+    if a.lib:
+        from revel_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     t0 = time.time()
     ctx = gpu.GpuContext(0)
     if a.image == "full":
@@ -119,7 +124,7 @@ def main():
         print(json.dumps({
             "workload": ("C3 zipf 64B-32KiB records (1 GiB written by the host writer, whole blocks tiled), device walk + segmented CRC verify"
                          if a.image == "zipf" else "C2-layout full blocks through the C3 verify path"),
-            "verify_variant": variant, "matches_production": same,
+            "verify_variant": variant, "matches_production": same, "lib": a.lib or "in-tree",
             "image_bytes": n, "blocks": nblocks, "physical_records": nrec, "bad_records": bad,
             "types": {int(t): int((res["type"] == t).sum()) for t in (1, 2, 3, 4)},
             "host_write_s": round(t_write, 2),
