@@ -300,10 +300,17 @@ __device__ void fill_inv_tree_tables(uint32_t* shtab, int levels) {
     }
 }
 // v * (the level-L constant of shtab), four unreplicated lookups.
+// acc ^ v * (the level-L constant): two 3-input xors.
+template <int L>
+__device__ __forceinline__ uint32_t tree_shift_xor(const uint32_t* shtab, uint32_t v, uint32_t acc) {
+    const uint32_t* t = shtab + L * 1024;
+    return __builtin_amdgcn_bitop3_b32(
+        __builtin_amdgcn_bitop3_b32(t[v & 0xffu], t[256 + ((v >> 8) & 0xffu)], t[512 + ((v >> 16) & 0xffu)], 0x96),
+        t[768 + (v >> 24)], acc, 0x96);
+}
 template <int L>
 __device__ __forceinline__ uint32_t tree_shift(const uint32_t* shtab, uint32_t v) {
-    const uint32_t* t = shtab + L * 1024;
-    return (t[v & 0xffu] ^ t[256 + ((v >> 8) & 0xffu)]) ^ (t[512 + ((v >> 16) & 0xffu)] ^ t[768 + (v >> 24)]);
+    return tree_shift_xor<L>(shtab, v, 0u);
 }
 
 template <int TM>
