@@ -47,8 +47,10 @@ constexpr uint32_t kListCap = 256;
 constexpr uint32_t kListStride = kListCap + 1;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st);
-// u64 words of a header-list buffer for nblocks: the lists, then the verify
-// kernel's list of qualifying blocks (a count and nblocks u32).
+// The verify kernel's list of qualifying blocks: kBlockListAux u32 of
+// counters (bucket totals, bucket cursors, the list length), then nblocks u32.
+constexpr uint32_t kBlockListAux = 2 * kListPerBlock + 1;
+// u64 words of a header-list buffer for nblocks: the lists, then the block list.
 uint64_t hlist_words(uint64_t nblocks);
 // d_tile_scratch: scan_scratch_words(n) u32 of device scratch.
 hipError_t exclusive_scan_u32(const DeviceInfo& di, const uint32_t* d_in, uint32_t* d_out, uint64_t n,
@@ -86,8 +88,8 @@ hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t 
 // at in-block offset lead) the number of records and the fragment index of
 // its first record, and one u64 header-list entry per fragment (written by
 // the scatter); with them the CRC pass reads its header lists instead of
-// walking the headers of every block.  d_blist: nblocks + 1 u32 of scratch for
-// the CRC pass's block list.
+// walking the headers of every block.  d_blist: kBlockListAux + nblocks u32 of
+// scratch for the CRC pass's block list.
 hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const FragDesc* d_frags, uint64_t nfrags,
                          void* d_image, uint64_t image_len, uint32_t lead, hipStream_t st,
                          const uint32_t* d_counts = nullptr, const uint32_t* d_first = nullptr,

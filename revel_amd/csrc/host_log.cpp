@@ -511,7 +511,7 @@ int revel_gpu_append_records(revel_gpu_context* ctx, const void* d_payloads, con
         if (e == hipSuccess) e = scratch.get(&d_counts, vblocks);
         if (e == hipSuccess) e = scratch.get(&d_first, vblocks);
         if (e == hipSuccess) e = scratch.get(&d_xlist, frags.size());
-        if (e == hipSuccess) e = scratch.get(&d_blist, vblocks + 1);
+        if (e == hipSuccess) e = scratch.get(&d_blist, vblocks + revel::kBlockListAux);
         if (e == hipSuccess) e = hipMemcpyAsync(d_counts, counts.data(), vblocks * 4, hipMemcpyHostToDevice, st);
         if (e == hipSuccess) e = hipMemcpyAsync(d_first, first.data(), vblocks * 4, hipMemcpyHostToDevice, st);
     }

@@ -44,10 +44,14 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
 // resuming at the offset the count pass left.  Entry k of block b goes into the
 // first 8 bytes of its own 24-byte result slot out[first[b] + k]: the verify
 // pass that covers record k reads it before it writes the result there.
+// It also zeroes the block-list counters (kBlockListAux u32 at zero_aux) the
+// verify launch's k_order_* kernels count into: one launch fewer than a memset.
 __global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbytes, const uint32_t* __restrict__ counts,
                                 const uint32_t* __restrict__ first, const uint64_t* __restrict__ hlist,
-                                revel_record_result* __restrict__ out) {
+                                revel_record_result* __restrict__ out, uint32_t* __restrict__ zero_aux) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (zero_aux && blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < kBlockListAux; i += blockDim.x) zero_aux[i] = 0;
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
          b += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t n = counts[b];
@@ -1037,7 +1041,7 @@ hipError_t exclusive_scan_u64(const DeviceInfo&, const uint64_t* d_in, uint64_t*
 
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
-uint64_t hlist_words(uint64_t nblocks) { return nblocks * kListStride + (nblocks + 2) / 2 + 1; }
+uint64_t hlist_words(uint64_t nblocks) { return nblocks * kListStride + (nblocks + kBlockListAux + 1) / 2 + 1; }
 
 // One-time per device (per thread): the x^(8d) / init_xor(d) tables.
 static hipError_t ensure_len_tables(const DeviceInfo& di, hipStream_t st) {
@@ -1114,23 +1118,17 @@ template <bool FRAME, bool ROWS = true, bool TQ = false, bool R64 = false, bool 
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
-                                      hipStream_t st, uint32_t* d_blist = nullptr) {
+                                      hipStream_t st, uint32_t* d_blist = nullptr, bool aux_zeroed = false) {
     const uint64_t vbytes = nbytes + lead;
     const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;
     if (b_hi > b_lo) {
         if constexpr (ROWS) {
-            // qualifying blocks listed first (d_blist[0] = count, then the list)
-            hipError_t e = hipMemsetAsync(d_blist, 0, 4, st);
-            if (e != hipSuccess) return e;
-            const uint64_t nb = b_hi - b_lo;
-            const uint64_t per_wg = kSparseThreads * kSparsePer;
-            hipLaunchKernelGGL(k_sparse_blocks,
-                               dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nb + per_wg - 1) / per_wg))),
-                               dim3(kSparseThreads), 0, st, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist + 1, d_blist);
-            e = hipGetLastError();
+            // qualifying blocks listed first, most records first (block_order)
+            hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, aux_zeroed, st);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
-                               img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + 1, d_blist);
+                               img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + kBlockListAux,
+                               d_blist + 2 * kListPerBlock);
         } else {
             const uint64_t waves = kVerify2Threads / 64;
             const uint32_t grid = (uint32_t)std::max<uint64_t>(
@@ -1175,7 +1173,7 @@ hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_ima
         // list the headers of blocks with more than kListCap records
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
         hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, counts, d_first, hl,
-                           d_out);
+                           d_out, path == 0 ? block_list(hl, nblocks) : nullptr);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1183,7 +1181,8 @@ hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_ima
     if (path == 0 && hl && counts && aligned16(img))
         return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts,
                                           reinterpret_cast<const uint64_t*>(d_out),
-                                          (uint32_t)(sizeof(revel_record_result) / 8), st, block_list(hl, nblocks));
+                                          (uint32_t)(sizeof(revel_record_result) / 8), st, block_list(hl, nblocks),
+                                          true);
     return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts, st);
 }
 

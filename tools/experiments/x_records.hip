@@ -45,15 +45,11 @@ hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t 
     const uint64_t b_hi = nbytes / kBlockSize;
     uint32_t* d_blist = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(hl) + nblocks * kListStride);
     if (b_hi) {
-        hipError_t e = hipMemsetAsync(d_blist, 0, 4, st);
+        hipError_t e = launch_block_order(di, d_counts, 0u, (uint32_t)b_hi, d_blist, false, st);
         if (e != hipSuccess) return e;
-        const uint64_t per_wg = kSparseThreads * kSparsePer;
-        hipLaunchKernelGGL(k_sparse_blocks,
-                           dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (b_hi + per_wg - 1) / per_wg))),
-                           dim3(kSparseThreads), 0, st, d_counts, 0u, (uint32_t)b_hi, d_blist + 1, d_blist);
         hipLaunchKernelGGL((k_verify_rows<false, RING, THREADS, DIAG, NB>), dim3((uint32_t)std::max(1, di.num_cu)),
-                           dim3(THREADS), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl, d_blist + 1,
-                           d_blist);
+                           dim3(THREADS), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl,
+                           d_blist + kBlockListAux, d_blist + 2 * kListPerBlock);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -81,7 +77,7 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
     if (hl && d_counts) {
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
         hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
-                           d_out);
+                           d_out, nullptr);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -207,4 +203,30 @@ extern "C" __attribute__((visibility("default"))) int revel_x_verify_records_var
     ctx->hlist_image = nullptr;
     if (e == hipErrorInvalidValue) return REVEL_INVALID_ARGUMENT;
     return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
+
+// Block-order experiment: k_verify_rows alone over a caller-built list of
+// qualifying blocks (d_list[0] = count, then block indices), so the order the
+// waves take blocks in (wave j: list[j], list[j + W], ...) can be measured.
+// Uses the header lists of the context's last count pass; dense and partial
+// blocks are not touched.  revel_x_rows_waves gives W.
+extern "C" __attribute__((visibility("default"))) int revel_x_rows_waves(revel_gpu_context* ctx) {
+    return ctx ? std::max(1, ctx->di.num_cu) * (kRowsThreads / 64) : 0;
+}
+extern "C" __attribute__((visibility("default"))) int revel_x_verify_rows_list(
+    revel_gpu_context* ctx, const void* d_image, size_t nbytes, const uint32_t* d_first, revel_record_result* d_out,
+    const uint32_t* d_list, void* stream) {
+    if (!ctx || !d_image || !d_first || !d_out || !d_list) return REVEL_INVALID_ARGUMENT;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    if (!(ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes)) return REVEL_INVALID_ARGUMENT;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = revel::ensure_len_tables(ctx->di, st);
+    if (e != hipSuccess) return REVEL_IO_ERROR;
+    hipLaunchKernelGGL((k_verify_rows<false, kRowsRing>), dim3((uint32_t)std::max(1, ctx->di.num_cu)),
+                       dim3(kRowsThreads), 0, st, static_cast<const uint8_t*>(d_image), (uint64_t)0, d_first,
+                       d_out, 0u, ctx->hlist, ctx->hlist_counts, reinterpret_cast<const uint64_t*>(d_out), d_list + 1,
+                       d_list);
+    ctx->hlist_image = nullptr;
+    return hipGetLastError() == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
 }
