@@ -23,7 +23,11 @@ def main():
     ap.add_argument("--variants", default="100,0,1,2,3,4,5,6,7")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="load this build of librevel_wal.so (A/B of two builds)")
     args = ap.parse_args()
+    if args.lib:
+        from revel_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     n = args.blocks
     variants = [int(v) for v in args.variants.split(",")]
     ctx = gpu.GpuContext(0)
