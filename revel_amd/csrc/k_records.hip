@@ -178,6 +178,9 @@ __device__ uint32_t g_init_xor_tab[kBlockSize + 1];
 
 // x^(-8d) for d = 0..32768 (filled with the x^(8d) / init_xor tables).
 __device__ uint32_t g_x8inv_tab[kBlockSize + 1];
+// k_verify_rows' six inverse-shift tree levels (fill_inv_tree_tables layout),
+// computed once here: the kernel copies them instead of 6 GF(2) multiplies per thread.
+__device__ uint32_t g_shtab[6 * 1024];
 
 struct InvShiftTables {
     uint32_t chunk[65];  // x^(-8*512*m)
@@ -214,6 +217,7 @@ __global__ void k_init_len_tables() {
         g_x8n_tab[d] = x;
         g_init_xor_tab[d] = gf_mul(x, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         g_x8inv_tab[d] = gf_x8inv_block(d);
+        if (d < 6u * 1024u) g_shtab[d] = gf_mul(c_inv_tree.c[d >> 10], (d & 255u) << (8u * ((d >> 8) & 3u)));
     }
 }
 
