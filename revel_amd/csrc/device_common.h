@@ -285,10 +285,15 @@ static_assert(multmodp(make_inv_tree().c[0], x8n(4)) == 0x80000000u, "inverse sh
 
 // S4R image of a gap table set (128 KiB, replicated 32x):
 // byte0 -> T''3 (r0 h0), byte1 -> T''2 (r0 h1), byte2 -> T''1 (r1 h0), byte3 -> T''0 (r1 h1)
+// Four words per ds_write_b128 (the 32 copies of an entry are consecutive
+// words, so a 16-B group holds one value): a quarter of the loads and LDS
+// writes of a word-by-word fill.  tab must be 16-B aligned.
 __device__ void fill_gap_tables(uint32_t* tab, const GapTables& g) {
-    for (uint32_t d = threadIdx.x; d < 32768u; d += blockDim.x) {
+    for (uint32_t q = threadIdx.x; q < 8192u; q += blockDim.x) {
+        const uint32_t d = 4u * q;
         const uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
-        tab[d] = g.t[3 - (r * 2 + h)][e];
+        const uint32_t v = g.t[3 - (r * 2 + h)][e];
+        reinterpret_cast<uint4*>(tab)[q] = make_uint4(v, v, v, v);
     }
 }
 // Inverse-shift tables, `levels` x 4 KiB unreplicated: level L, byte k, entry e at

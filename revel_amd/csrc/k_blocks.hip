@@ -103,7 +103,7 @@ template <int THREADS, bool FRAME>
 __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                           uint32_t* __restrict__ masked_out,
                                                           uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
-    __shared__ uint32_t tab[32768];      // 128 KiB: T'' replicated 32x
+    __shared__ alignas(16) uint32_t tab[32768];  // 128 KiB: T'' replicated 32x
     __shared__ uint32_t shtab[8 * 1024];  // 32 KiB: inverse-shift tree tables
     fill_gap_tables(tab, c_gap1020);
     fill_inv_tree_tables(shtab, 8);
