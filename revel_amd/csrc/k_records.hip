@@ -1097,14 +1097,15 @@ template <bool FRAME>
 static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes,
                                            uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                            uint32_t lead, const uint64_t* hl, const uint32_t* d_counts,
-                                           const uint64_t* xl, uint32_t xs, hipStream_t st) {
+                                           const uint64_t* xl, uint32_t xs, hipStream_t st,
+                                           const uint32_t* dense_whole = nullptr) {
     const uint64_t vbytes = nbytes + lead;
     const uint64_t nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
     const uint64_t waves = kDenseThreads / 64;
     const uint32_t grid =
         (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     hipLaunchKernelGGL(k_verify_records_dense<FRAME>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
-                       d_first, d_out, lead, hl, d_counts, xl, xs);
+                       d_first, d_out, lead, hl, d_counts, xl, xs, dense_whole);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || (lead == 0 && vbytes % kBlockSize == 0)) return e;
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st, img,
@@ -1125,6 +1126,7 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
                                       hipStream_t st, uint32_t* d_blist = nullptr, bool aux_zeroed = false) {
     const uint64_t vbytes = nbytes + lead;
     const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;
+    const uint32_t* dense_whole = nullptr;  // counted by k_order_hist when it runs
     if (b_hi > b_lo) {
         if constexpr (ROWS) {
             // qualifying blocks listed first, most records first (block_order)
@@ -1133,6 +1135,7 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
             hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + kBlockListAux,
                                d_blist + 2 * kListPerBlock);
+            dense_whole = d_blist + 2 * kListPerBlock + 1;
         } else {
             const uint64_t waves = kVerify2Threads / 64;
             const uint32_t grid = (uint32_t)std::max<uint64_t>(
@@ -1144,7 +1147,8 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    return launch_dense_and_partial<FRAME>(di, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, st);
+    return launch_dense_and_partial<FRAME>(di, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, st,
+                                           dense_whole);
 }
 
 // the dense kernel reads aligned 16 B relative to the image start
