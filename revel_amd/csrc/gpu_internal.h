@@ -47,10 +47,11 @@ constexpr uint32_t kListCap = 256;
 constexpr uint32_t kListStride = kListCap + 1;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st);
-// The verify kernel's list of qualifying blocks: kBlockListAux u32 of
-// counters (bucket totals, bucket cursors, the list length, the number of
-// dense whole blocks), then nblocks u32.
-constexpr uint32_t kBlockListAux = 2 * kListPerBlock + 2;
+// The verify kernel's list of qualifying blocks: kBlockListAux u32 (the list
+// length, the number of dense blocks, one row of kListPerBlock + 1 bucket
+// counts per workgroup of the ordering kernels), then nblocks u32.
+constexpr uint32_t kOrderMaxWG = 256;
+constexpr uint32_t kBlockListAux = 2 + kOrderMaxWG * (kListPerBlock + 1);
 // u64 words of a header-list buffer for nblocks: the lists, then the block list.
 uint64_t hlist_words(uint64_t nblocks);
 // d_tile_scratch: scan_scratch_words(n) u32 of device scratch.

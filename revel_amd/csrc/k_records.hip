@@ -39,36 +39,6 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 
-// Header-list entries of records kListCap.. of the blocks that have more
-// (small-record logs: a 131-B record gives ~250 per block), one lane per block,
-// resuming at the offset the count pass left.  Entry k of block b goes into the
-// first 8 bytes of its own 24-byte result slot out[first[b] + k]: the verify
-// pass that covers record k reads it before it writes the result there.
-// It also zeroes the block-list counters (kBlockListAux u32 at zero_aux) the
-// verify launch's k_order_* kernels count into: one launch fewer than a memset.
-__global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbytes, const uint32_t* __restrict__ counts,
-                                const uint32_t* __restrict__ first, const uint64_t* __restrict__ hlist,
-                                revel_record_result* __restrict__ out, uint32_t* __restrict__ zero_aux) {
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    if (zero_aux && blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < kBlockListAux; i += blockDim.x) zero_aux[i] = 0;
-    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
-         b += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t n = counts[b];
-        if (n <= kListCap) continue;
-        const uint64_t base = b * kBlockSize;
-        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
-        const uint8_t* blk = image + base;
-        uint32_t off = (uint32_t)hlist[b * kListStride + kListCap];
-        uint64_t* slot = reinterpret_cast<uint64_t*>(out + first[b]);
-        for (uint32_t k = kListCap; k < n; ++k) {
-            const Hdr h = read_header(blk, off, bl);
-            slot[k * (sizeof(revel_record_result) / 8)] = list_entry(h);
-            off += kHeaderSize + h.len;  // only the last record can be bad
-        }
-    }
-}
-
 // Exclusive scan in two parallel passes over tiles of kScanTile elements
 // (256 threads x 4): k_tile_sums writes each tile's sum; k_scan_apply adds the
 // sums of the tiles before it and scans its own tile.
@@ -292,7 +262,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
                                                                      const uint64_t* __restrict__ hlist,
                                                                      const uint32_t* __restrict__ counts,
                                                                      const uint64_t* __restrict__ xlist = nullptr,
-                                                                     uint32_t xstride = 3) {
+                                                                     uint32_t xstride = 3, uint32_t skip_tail = 0) {
     __shared__ uint32_t tab[TableCfg<TM>::bytes / 4];
     __shared__ VerifyWaveLds2 wl_all[THREADS / 64];
     fill_tables<TM>(tab);
@@ -323,6 +293,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
         if constexpr (SPARSE_ONLY) {  // a dense partial block went to k_verify_records_dense
             if (counts[b] > kListPerBlock) continue;
         }
+        if (skip_tail && b != 0 && b == nblocks - 1) continue;  // k_verify_rows took the tail block
         const uint32_t cs = lane * 512u, ce = cs + 512u;
         uint32_t out_base = FRAME ? 0u : first[b];
         uint32_t walk_from = lo_b;
@@ -892,6 +863,24 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 
 #include "verify_dense.inc"
 #include "verify_rows.inc"
+
+// Header-list entries of records kListCap.. of the blocks that have more
+// (small-record logs: a 131-B record gives ~250 per block), one lane per block,
+// for the verify paths that do not order blocks (the split path walks them in
+// k_order_hist).  Entry k of block b goes into the first 8 bytes of its own
+// 24-byte result slot out[first[b] + k]: the verify pass that covers record k
+// reads it before it writes the result there.
+__global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbytes, const uint32_t* __restrict__ counts,
+                                const uint32_t* __restrict__ first, const uint64_t* __restrict__ hlist,
+                                revel_record_result* __restrict__ out) {
+    const OverflowArgs ov{image, nbytes, first, hlist, out};
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t n = counts[b];
+        if (n > kListCap) list_overflow_block(ov, b, n);
+    }
+}
 constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
 
 // ---------------------------------------------------------------------------
@@ -1098,7 +1087,7 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
                                            uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                            uint32_t lead, const uint64_t* hl, const uint32_t* d_counts,
                                            const uint64_t* xl, uint32_t xs, hipStream_t st,
-                                           const uint32_t* dense_whole = nullptr) {
+                                           const uint32_t* dense_whole = nullptr, bool tail_in_rows = false) {
     const uint64_t vbytes = nbytes + lead;
     const uint64_t nblocks = (vbytes + kBlockSize - 1) / kBlockSize;
     const uint64_t waves = kDenseThreads / 64;
@@ -1107,9 +1096,9 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
     hipLaunchKernelGGL(k_verify_records_dense<FRAME>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
                        d_first, d_out, lead, hl, d_counts, xl, xs, dense_whole);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || (lead == 0 && vbytes % kBlockSize == 0)) return e;
+    if (e != hipSuccess || (lead == 0 && (vbytes % kBlockSize == 0 || tail_in_rows))) return e;
     hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0, st, img,
-                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs);
+                       nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, tail_in_rows ? 1u : 0u);
     return hipGetLastError();
 }
 
@@ -1123,19 +1112,27 @@ template <bool FRAME, bool ROWS = true, bool TQ = false, bool R64 = false, bool 
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
-                                      hipStream_t st, uint32_t* d_blist = nullptr, bool aux_zeroed = false) {
+                                      hipStream_t st, uint32_t* d_blist = nullptr, const OverflowArgs* ov = nullptr) {
     const uint64_t vbytes = nbytes + lead;
-    const uint64_t b_lo = lead ? 1u : 0u, b_hi = vbytes / kBlockSize;
+    const uint64_t b_lo = lead ? 1u : 0u;
+    uint64_t b_hi = vbytes / kBlockSize;
     const uint32_t* dense_whole = nullptr;  // counted by k_order_hist when it runs
+    // A partial tail block (not also the lead block) joins the rows kernel's
+    // list when its 16-B groups are image-aligned: one single-wave launch fewer
+    // (~50 us of latency-bound walk per verify, profiles/r2_s4_partial_tail.txt).
+    const uint32_t tail_bl = (uint32_t)(vbytes % kBlockSize);
+    const bool tail_in_rows = ROWS && tail_bl != 0 && b_hi >= b_lo && lead % 16u == 0;
+    const uint32_t tail_block = tail_in_rows ? (uint32_t)b_hi : 0xFFFFFFFFu;
+    if (tail_in_rows) ++b_hi;
     if (b_hi > b_lo) {
         if constexpr (ROWS) {
             // qualifying blocks listed first, most records first (block_order)
-            hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, aux_zeroed, st);
+            hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, st, ov);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + kBlockListAux,
-                               d_blist + 2 * kListPerBlock);
-            dense_whole = d_blist + 2 * kListPerBlock + 1;
+                               d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize);
+            dense_whole = d_blist + 1;
         } else {
             const uint64_t waves = kVerify2Threads / 64;
             const uint32_t grid = (uint32_t)std::max<uint64_t>(
@@ -1148,7 +1145,7 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
         if (e != hipSuccess) return e;
     }
     return launch_dense_and_partial<FRAME>(di, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, st,
-                                           dense_whole);
+                                           dense_whole, tail_in_rows);
 }
 
 // the dense kernel reads aligned 16 B relative to the image start
@@ -1177,20 +1174,25 @@ hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_ima
     const uint64_t* hl = path == 1 ? nullptr : d_hlist;
     const uint32_t* counts = path == 1 ? nullptr : d_counts;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    const bool split = path == 0 && hl && counts && aligned16(img);
+    if (split) {
+        // k_order_hist lists the headers of blocks with more than kListCap
+        // records: its range is every block (lead 0, the partial tail included)
+        const OverflowArgs ov{img, nbytes, d_first, hl, d_out};
+        return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts,
+                                          reinterpret_cast<const uint64_t*>(d_out),
+                                          (uint32_t)(sizeof(revel_record_result) / 8), st, block_list(hl, nblocks),
+                                          &ov);
+    }
     if (hl && counts) {
         // list the headers of blocks with more than kListCap records
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
         hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, counts, d_first, hl,
-                           d_out, path == 0 ? block_list(hl, nblocks) : nullptr);
+                           d_out);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     const bool partial = nbytes % kBlockSize != 0;
-    if (path == 0 && hl && counts && aligned16(img))
-        return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts,
-                                          reinterpret_cast<const uint64_t*>(d_out),
-                                          (uint32_t)(sizeof(revel_record_result) / 8), st, block_list(hl, nblocks),
-                                          true);
     return launch_verify3<false>(grid, partial, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts, st);
 }
 

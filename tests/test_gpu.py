@@ -11,7 +11,7 @@ import pytest
 from revel_amd import BLOCK_SIZE, env, log
 from revel_amd._lib import IO_ERROR, RevelError
 from revel_amd.gpu import RECORD_DTYPE
-from conftest import golden_image
+from conftest import golden_image, trace
 from oracle import crc32c_oracle as po
 from oracle import oracle_c as oc
 
@@ -203,6 +203,69 @@ def test_verify_partial_last_block(gpu_ctx, cut, path):
     img = img[:min(len(img), cut + 65536)]
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
     compare_walk(gpu_ctx.verify_image(dimg, len(img), path=path), oc.walk(img))
+
+
+@pytest.mark.parametrize("tail_records", [1, 13, 63, 64, 65])
+def test_verify_tail_block_cuts(gpu_ctx, tail_records):
+    """The partial tail block goes through k_verify_rows with a length-bounded
+    buffer resource: cuts at record ends, inside headers and payloads, at and
+    around 16-B / 256-B / 1 KiB boundaries, a flipped bit in the tail; 64
+    records = the rows kernel's limit, 65 = the dense kernel."""
+    rng = np.random.default_rng(100 + tail_records)
+    head = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(500, 9000, 8)]
+    img0 = oc.write_image(head)
+    pad = (-len(img0)) % 32768
+    # fill to the block end with one record (or a trailer), then the tail records
+    filler = [bytes(rng.integers(0, 256, pad - 7, dtype=np.uint8))] if pad >= 7 else []
+    sizes = rng.integers(0, 380, tail_records)
+    tail = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    img = oc.write_image(head + filler + tail)
+    ends = oc.walk(img)
+    base = (len(img) - 1) // 32768 * 32768
+    rec_ends = [int(o) + 7 + int(n) for o, n in zip(ends["file_offset"], ends["length"]) if o >= base]
+    cuts = set(rec_ends[-3:]) | {e - 1 for e in rec_ends[-3:]} | {e - 5 for e in rec_ends[-2:]}
+    cuts |= {base + k for k in (1, 6, 7, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025)}
+    for cut in sorted(c for c in cuts if base < c <= len(img)):
+        part = bytearray(img[:cut])
+        if cut == len(img) and len(rec_ends) > 2:
+            part[rec_ends[-2] - 3] ^= 0x10  # a payload bit of the second-to-last tail record
+        part = bytes(part)
+        dimg = gpu_ctx.upload(np.frombuffer(part, dtype=np.uint8))
+        compare_walk(gpu_ctx.verify_image(dimg, len(part)), oc.walk(part))
+        dimg.free()
+
+
+@pytest.mark.parametrize("trailer", [0, 3, 6])
+def test_verify_and_append_64_record_blocks(gpu_ctx, trailer):
+    """Whole blocks with exactly 64 records (the rows kernel's limit: the end
+    capture has no lane of its own), the last one ending `trailer` bytes before
+    the block end, through verify and device append framing, plus a flipped
+    bit in record 63."""
+    rng = np.random.default_rng(640 + trailer)
+    recs = []
+    for _ in range(3):
+        body = 32768 - trailer - 64 * 7
+        cuts = np.sort(rng.choice(np.arange(1, body), 63, replace=False))
+        sizes = np.diff(np.concatenate([[0], cuts, [body]]))
+        recs += [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    img = oc.write_image(recs)
+    assert len(img) == 3 * 32768 - trailer  # the writer leaves the last trailer out
+    ref = oc.walk(img)
+    assert len(ref) == 192
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    compare_walk(gpu_ctx.verify_image(dimg, len(img)), ref)
+    bad = bytearray(img)
+    bad[int(ref["file_offset"][63]) + 9] ^= 4
+    bad = bytes(bad)
+    dbad = gpu_ctx.upload(np.frombuffer(bad, dtype=np.uint8))
+    res = gpu_ctx.verify_image(dbad, len(bad))
+    compare_walk(res, oc.walk(bad))
+    assert np.flatnonzero(res["status"] == 1).tolist() == [63]
+    blob = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    d = gpu_ctx.upload(blob)
+    out, n, _ = gpu_ctx.append_records(d, [len(r) for r in recs], 0)
+    assert n == len(img)
+    assert gpu_ctx.d2h(out, n).tobytes() == img
 
 
 def test_verify_small_records_dense(gpu_ctx):

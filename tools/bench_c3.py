@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--variants", default="0,15")
     ap.add_argument("--lib", default=None,
                     help="load this build of librevel_wal.so instead of the in-tree one (A/B of two builds)")
+    ap.add_argument("--keep-tail", action="store_true",
+                    help="end the tiled image with the writer's partial last block (as bench.py's c3 image does)")
     ap.add_argument("--image", choices=["zipf", "full"], default="zipf",
                     help="full = C2-style full blocks (1 record/block): the verify kernels' base cost")
     a = ap.parse_args()
@@ -73,7 +75,7 @@ def main():
         img = make_image(a.bytes)
         if a.tile > 1:  # whole blocks only, so the tiles stay block-aligned
             whole = len(img) // BLOCK_SIZE * BLOCK_SIZE
-            img = img[:whole] * a.tile
+            img = img[:whole] * (a.tile - 1) + (img if a.keep_tail else img[:whole])
         n = len(img)
         d = ctx.upload(np.frombuffer(img, dtype=np.uint8))
     t_write = time.time() - t0
@@ -122,7 +124,8 @@ def main():
         same = same_all[variant]
         ta, tv = float(np.median(times_all)), float(np.median(times_verify))
         print(json.dumps({
-            "workload": ("C3 zipf 64B-32KiB records (1 GiB written by the host writer, whole blocks tiled), device walk + segmented CRC verify"
+            "workload": ("C3 zipf 64B-32KiB records (1 GiB written by the host writer, whole blocks tiled"
+                         + (", partial tail block kept" if a.keep_tail else "") + "), device walk + segmented CRC verify"
                          if a.image == "zipf" else "C2-layout full blocks through the C3 verify path"),
             "verify_variant": variant, "matches_production": same, "lib": a.lib or "in-tree",
             "image_bytes": n, "blocks": nblocks, "physical_records": nrec, "bad_records": bad,

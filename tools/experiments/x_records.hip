@@ -45,11 +45,11 @@ hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t 
     const uint64_t b_hi = nbytes / kBlockSize;
     uint32_t* d_blist = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(hl) + nblocks * kListStride);
     if (b_hi) {
-        hipError_t e = launch_block_order(di, d_counts, 0u, (uint32_t)b_hi, d_blist, false, st);
+        hipError_t e = launch_block_order(di, d_counts, 0u, (uint32_t)b_hi, d_blist, st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_verify_rows<false, RING, THREADS, DIAG, NB>), dim3((uint32_t)std::max(1, di.num_cu)),
                            dim3(THREADS), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl,
-                           d_blist + kBlockListAux, d_blist + 2 * kListPerBlock);
+                           d_blist + kBlockListAux, d_blist);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -77,7 +77,7 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
     if (hl && d_counts) {
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
         hipLaunchKernelGGL(k_list_overflow, dim3((uint32_t)g), dim3(64), 0, st, img, nbytes, d_counts, d_first, hl,
-                           d_out, nullptr);
+                           d_out);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
