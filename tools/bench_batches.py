@@ -100,7 +100,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="another build of librevel_wal.so (A/B)")
     a = ap.parse_args()
+    if a.lib:
+        from revel_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     ctx = gpu.GpuContext(0)
     for name, per in [("fill1", 1), ("fill100", 100)]:
         print(json.dumps(run(ctx, name, per, a.bytes, a.iters)), flush=True)
