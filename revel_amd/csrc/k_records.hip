@@ -13,8 +13,18 @@
 using namespace revel;
 
 namespace {
-// Per block (one lane each): number of physical records and, when list is
-// non-null, the first kListCap headers (list_entry; the walk stops at the
+// The 7 header bytes at byte sh (0..5) of a 12-byte window w.
+__device__ __forceinline__ Hdr header_in_window(uint3 w, uint32_t sh) {
+    const uint32_t r = sh & 3u;
+    const bool hi = sh >= 4u;
+    const uint32_t lo0 = hi ? w.y : w.x, lo1 = hi ? w.z : w.y, lo2 = hi ? 0u : w.z;
+    const uint32_t a = __builtin_amdgcn_alignbyte(lo1, lo0, r);  // bytes sh..sh+3
+    const uint32_t b = __builtin_amdgcn_alignbyte(lo2, lo1, r);  // bytes sh+4..sh+7
+    return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
+}
+
+// Per block (one lane each): number of physical records and the first
+// kListCap headers (list_entry; the walk stops at the
 // first bad header, so only the last entry can be bad) followed by the in-block
 // offset of record kListCap when the block has more records.
 __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts,
@@ -25,15 +35,39 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
         const uint64_t base = b * kBlockSize;
         const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
         const uint8_t* blk = image + base;
-        uint32_t off = 0, n = 0;
-        while (bl - off >= kHeaderSize) {
-            const Hdr h = read_header(blk, off, bl);
-            const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-            if (hlist && n < kListCap) hlist[b * kListStride + n] = list_entry(h);
-            if (hlist && n == kListCap) hlist[b * kListStride + kListCap] = off;  // resume point
-            ++n;
-            if (!ok) break;
-            off += kHeaderSize + h.len;
+        uint32_t n = 0;
+        if (bl >= 12u) {
+            // The next header's 12 B are loaded unconditionally, before this
+            // header's list store: loads and stores share vmcnt, so a store
+            // issued first would put its completion into every hop of the
+            // dependent walk.  Window address a = min(off & ~3, bl - 12): a window
+            // never reaches past the block (or the image end), and off - a <= 5
+            // keeps the 7 header bytes inside it.
+            const uint32_t cap = bl - 12u;
+            uint32_t off = 0, a = 0, resume = 0;
+            uint3 w = *reinterpret_cast<const uint3*>(blk);
+            for (;;) {
+                const Hdr h = header_in_window(w, off - a);
+                const bool ok = classify(h, off, bl) == REVEL_REC_OK;
+                const uint32_t next = off + kHeaderSize + h.len;  // <= bl when ok
+                const bool more = ok && bl - next >= kHeaderSize;
+                const uint32_t an = min(more ? next & ~3u : 0u, cap);
+                const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
+                // one unconditional store per hop (a store in a branch makes the
+                // compiler wait for it at the merge): entry n, or from record
+                // kListCap on the resume offset (rewritten with the same value)
+                resume = n == kListCap ? off : resume;
+                hlist[b * kListStride + min(n, kListCap)] = n < kListCap ? list_entry(h) : uint64_t(resume);
+                ++n;
+                if (!more) break;
+                off = next;
+                a = an;
+                w = wn;
+            }
+        } else if (bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
+            const Hdr h = read_header(blk, 0u, bl);
+            hlist[b * kListStride] = list_entry(h);
+            n = 1;
         }
         counts[b] = n;
     }
