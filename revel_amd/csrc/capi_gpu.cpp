@@ -54,6 +54,7 @@ void destroy_context(revel_gpu_context* ctx) {
     }
     if (ctx->hlist) (void)hipFree(ctx->hlist);
     if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
+    if (ctx->wsums) (void)hipFree(ctx->wsums);
     if (ctx->arena.base) (void)hipFree(ctx->arena.base);
     auto& pr = ctx->parked_reader;
     if (pr.h_win) (void)hipHostFree(pr.h_win);
@@ -253,8 +254,18 @@ int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t 
                 "hipMalloc(header list)");
         ctx->hlist_cap_blocks = nblocks;
     }
-    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, ctx->hlist, pick(ctx, stream)),
+    const uint64_t nw = revel::count_wave_sums(nblocks);
+    if (nw > ctx->wsums_cap) {
+        if (ctx->wsums) (void)hipFree(ctx->wsums);
+        ctx->wsums = nullptr;
+        ctx->wsums_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->wsums), nw * sizeof(uint32_t)), "hipMalloc(wave sums)");
+        ctx->wsums_cap = nw;
+    }
+    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, ctx->hlist, pick(ctx, stream), ctx->wsums),
             "count_records launch");
+    ctx->wsums_counts = d_counts;
+    ctx->wsums_n = nblocks;
     ctx->hlist_image = d_image;
     ctx->hlist_nbytes = nbytes;
     ctx->hlist_counts = d_counts;
@@ -266,6 +277,13 @@ int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, u
     CHECK_CTX(ctx);
     if (n == 0) return REVEL_OK;
     if (!d_in || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    if (ctx->wsums_counts == d_in && ctx->wsums_n == n) {
+        // the counts of the last count pass: its per-64-block sums are the
+        // scan's first pass (one launch instead of two)
+        ctx->wsums_counts = nullptr;
+        HIP_TRY(revel::exclusive_scan_counts(ctx->di, d_in, d_out, n, ctx->wsums, pick(ctx, stream)), "scan launch");
+        return REVEL_OK;
+    }
     const uint64_t words = revel::scan_scratch_words(n);
     if (words > ctx->scan_scratch_cap) {
         if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);

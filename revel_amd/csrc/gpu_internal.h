@@ -46,7 +46,13 @@ constexpr uint32_t kListPerBlock = 64;
 constexpr uint32_t kListCap = 256;
 constexpr uint32_t kListStride = kListCap + 1;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                         uint64_t* d_hlist, hipStream_t st);
+                         uint64_t* d_hlist, hipStream_t st, uint32_t* d_wsums = nullptr);
+// With d_wsums (count_wave_sums(nblocks) u32), the count pass also leaves the
+// records per 64 blocks; exclusive_scan_counts turns them and the counts into
+// the exclusive scan in one launch.
+uint64_t count_wave_sums(uint64_t nblocks);
+hipError_t exclusive_scan_counts(const DeviceInfo& di, const uint32_t* d_counts, uint32_t* d_first, uint64_t nblocks,
+                                 const uint32_t* d_wsums, hipStream_t st);
 // The verify kernel's list of qualifying blocks: kBlockListAux u32 (the list
 // length, the number of dense blocks, one row of kListPerBlock + 1 bucket
 // counts per workgroup of the ordering kernels), then nblocks u32.
@@ -223,6 +229,12 @@ struct revel_gpu_context {
     const uint32_t* hlist_counts = nullptr;
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
+    // per-64-block record sums of the last count pass (revel_gpu_count_records),
+    // consumed by the next revel_gpu_exclusive_scan_u32 of exactly those counts
+    uint32_t* wsums = nullptr;
+    uint64_t wsums_cap = 0;
+    const uint32_t* wsums_counts = nullptr;  // the counts they sum (nullptr: none pending)
+    uint64_t wsums_n = 0;
     revel::ScratchArena arena;  // per-call scratch of decode_batches / reassemble / append framing
     // Window buffers of the last revel_log_reader freed on this context, parked
     // for the next reader with the same window (host_log.cpp): a reader per log

@@ -27,15 +27,20 @@ __device__ __forceinline__ Hdr header_in_window(uint3 w, uint32_t sh) {
 // kListCap headers (list_entry; the walk stops at the
 // first bad header, so only the last entry can be bad) followed by the in-block
 // offset of record kListCap when the block has more records.
-__global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes, uint32_t* __restrict__ counts,
-                                uint64_t* __restrict__ hlist) {
+// With wsums (one wave per workgroup), wsums[w] = the records of blocks
+// [64 w, 64 w + 64): the first pass of the exclusive scan that follows
+// (revel_gpu_exclusive_scan_u32 on these counts skips its tile-sum launch).
+__global__ __launch_bounds__(64) void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                                      uint32_t* __restrict__ counts, uint64_t* __restrict__ hlist,
+                                                      uint32_t* __restrict__ wsums) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
-         b += (uint64_t)gridDim.x * blockDim.x) {
+    for (uint64_t b0 = blockIdx.x * 64ull; b0 < nblocks; b0 += gridDim.x * 64ull) {  // wave-uniform
+        const uint64_t b = b0 + threadIdx.x;
+        uint32_t n = 0;
+        if (b < nblocks) {
         const uint64_t base = b * kBlockSize;
         const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
         const uint8_t* blk = image + base;
-        uint32_t n = 0;
         if (bl >= 12u) {
             // The next header's 12 B are loaded unconditionally, before this
             // header's list store: loads and stores share vmcnt, so a store
@@ -70,6 +75,13 @@ __global__ void k_count_records(const uint8_t* __restrict__ image, uint64_t nbyt
             n = 1;
         }
         counts[b] = n;
+        }
+        if (wsums) {
+            uint32_t t = n;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m, 64);
+            if (threadIdx.x == 0) wsums[b0 / 64u] = t;
+        }
     }
 }
 
@@ -103,14 +115,16 @@ __global__ __launch_bounds__(256) void k_tile_sums(const T* __restrict__ in, uin
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = t;
 }
 
-template <typename T>
+// PARTS = partial sums per tile in `tile_sums` (1: k_tile_sums; kScanTile / 64:
+// the per-wave sums of k_count_records).
+template <typename T, uint32_t PARTS = 1>
 __global__ __launch_bounds__(256) void k_scan_apply(const T* __restrict__ in, uint64_t n, const T* __restrict__ tile_sums,
                                                     T* __restrict__ out) {
     __shared__ T red[4];
     __shared__ T wsum[4];
-    // offset of this tile = sum of the tile sums before it
+    // offset of this tile = sum of the partial sums before it
     T pre = 0;
-    for (uint32_t t = threadIdx.x; t < blockIdx.x; t += 256) pre += tile_sums[t];
+    for (uint32_t t = threadIdx.x; t < blockIdx.x * PARTS; t += 256) pre += tile_sums[t];
     const T tile_off = block_reduce_256<T>(pre, red);
     // each thread owns 4 consecutive elements
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
@@ -1036,12 +1050,23 @@ __global__ void k_summary_blocks(const uint8_t* __restrict__ ok, uint64_t nblock
 
 namespace revel {
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                         uint64_t* d_hlist, hipStream_t st) {
+                         uint64_t* d_hlist, hipStream_t st, uint32_t* d_wsums) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     // one lane per block: every header chain walks concurrently
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, (nblocks + 63) / 64));
     hipLaunchKernelGGL(k_count_records, dim3((uint32_t)grid), dim3(64), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist);
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_wsums);
+    return hipGetLastError();
+}
+
+uint64_t count_wave_sums(uint64_t nblocks) { return (nblocks + 63) / 64; }
+
+hipError_t exclusive_scan_counts(const DeviceInfo&, const uint32_t* d_counts, uint32_t* d_first, uint64_t nblocks,
+                                 const uint32_t* d_wsums, hipStream_t st) {
+    if (nblocks == 0) return hipSuccess;
+    const uint64_t tiles = (nblocks + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL((k_scan_apply<uint32_t, kScanTile / 64>), dim3((uint32_t)tiles), dim3(256), 0, st, d_counts,
+                       nblocks, d_wsums, d_first);
     return hipGetLastError();
 }
 
