@@ -228,7 +228,11 @@ int revel_gpu_frame_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t n
  * of the same image on the same context uses them (for blocks with more than
  * 64 records it first lists the rest into their own d_out slots, which it
  * then overwrites with the results); without them verify walks the headers
- * itself, with the same results, slower. */
+ * itself, with the same results, slower.  It also leaves the records per 64
+ * blocks: the next revel_gpu_exclusive_scan_u32 of exactly that d_counts array
+ * and n = its block count, before anything writes d_counts, uses them as its
+ * first pass (one launch instead of two); any other scan takes the general
+ * path. */
 int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,
                             uint32_t* d_counts, void* stream);
 int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, uint32_t* d_out,
