@@ -603,6 +603,40 @@ def test_exclusive_scan(gpu_ctx, n):
     assert np.array_equal(gpu_ctx.d2h(dout, 4 * n, np.uint32), want)
 
 
+@pytest.mark.parametrize("nblocks", [1, 63, 64, 65, 1023, 1024, 1025, 4100])
+def test_scan_of_counts_after_count_pass(gpu_ctx, nblocks):
+    """The scan right after a count pass of the same counts uses the count
+    pass's per-64-block sums (one launch); a second scan of them, a scan of a
+    prefix, and a scan after another count pass take the general path.  All
+    equal the oracle walk's per-block record counts scanned on the host."""
+    from revel_amd._lib import check, lib
+    L = lib()
+    rng = np.random.default_rng(nblocks)
+    sizes = rng.integers(0, 3000, nblocks * 24)
+    recs = [bytes(int(s)) for s in sizes]
+    img = oc.write_image(recs)[:nblocks * BLOCK_SIZE - int(rng.integers(0, 100))]
+    assert (len(img) + BLOCK_SIZE - 1) // BLOCK_SIZE == nblocks
+    nb = (len(img) + BLOCK_SIZE - 1) // BLOCK_SIZE
+    ref = oc.walk(img)
+    want_counts = np.bincount(ref["file_offset"] // BLOCK_SIZE, minlength=nb).astype(np.uint32)
+    want = np.concatenate([[0], np.cumsum(want_counts, dtype=np.uint64)[:-1]]).astype(np.uint32)
+    d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    counts, first, first2 = gpu_ctx.alloc(4 * nb), gpu_ctx.alloc(4 * nb), gpu_ctx.alloc(4 * nb)
+    check(L.revel_gpu_count_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, None))
+    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first.ptr, nb, None))   # one launch
+    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first2.ptr, nb, None))  # general
+    gpu_ctx.sync()
+    assert np.array_equal(gpu_ctx.d2h(counts, 4 * nb, np.uint32), want_counts)
+    assert np.array_equal(gpu_ctx.d2h(first, 4 * nb, np.uint32), want)
+    assert np.array_equal(gpu_ctx.d2h(first2, 4 * nb, np.uint32), want)
+    # a prefix of the counts right after a count pass: general path
+    check(L.revel_gpu_count_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, None))
+    k = max(1, nb // 2)
+    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first2.ptr, k, None))
+    gpu_ctx.sync()
+    assert np.array_equal(gpu_ctx.d2h(first2, 4 * k, np.uint32), want[:k])
+
+
 # ---- device replay reassembly vs the oracle reader's event sequence ----
 def check_reassembly(gpu_ctx, img, checksum=True):
     d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
