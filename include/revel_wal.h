@@ -180,6 +180,15 @@ int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t ini
  * *data == NULL (the reference returns an empty Slice, :140).  A checksum
  * mismatch returns REVEL_IO_ERROR, as the reference does (:142-152). */
 int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size_t* n);
+/* log_reader.rs:76 with the reference's ownership: the record is written into
+ * the caller's scratch (buf, cap) -- the `&mut Vec<u8>` the returned Slice
+ * borrows -- and *n receives its length.  When cap is short the call returns
+ * REVEL_INVALID_ARGUMENT with *n = the bytes needed and keeps the record: the
+ * next read call (after the caller grows its scratch) returns it.  End of
+ * file: REVEL_OK, *n == 0 and *eof = 1 (eof may be NULL: the reference's empty
+ * Slice, :140, does not tell EOF from an empty record either).  Fragments are
+ * assembled straight into buf while they fit, so a record is copied once. */
+int revel_log_reader_read_record_into(revel_log_reader* r, uint8_t* buf, size_t cap, size_t* n, int* eof);
 /* File offset of the first physical record of the last returned record. */
 uint64_t revel_log_reader_last_record_offset(const revel_log_reader* r);
 void revel_log_reader_free(revel_log_reader* r);

@@ -190,13 +190,29 @@ def full_block_masked_crcs(blocks: np.ndarray) -> np.ndarray:
 
 # --- Writer (log_writer.rs:25-124) ------------------------------------------
 class LogWriter:
-    """Restatement of ``log_writer::Writer`` writing into a bytearray."""
+    """Restatement of ``log_writer::Writer`` writing into a bytearray, or into
+    ``file`` -- any object with ``append(bytes)`` and ``flush()`` (the
+    ``dyn WritableFile`` of env.rs:40-50) whose calls may raise.  A raising
+    call propagates out of ``add_record`` at the point the reference's ``?``
+    returns (log_writer.rs:70, :91, :114-119): the bytes already appended stay
+    in the file and ``block_offset`` keeps the value it had at that point."""
 
-    def __init__(self, dest: Optional[bytearray] = None, block_offset: int = 0):
+    def __init__(self, dest: Optional[bytearray] = None, block_offset: int = 0, file=None):
         # log_writer.rs:45-53: block_offset is taken as given (no % kBlockSize)
         self.dest = dest if dest is not None else bytearray()
+        self.file = file
         self.block_offset = block_offset
         self.type_crc = list(range(MAX_RECORD_TYPE + 1))  # init_type_crc, :33-37
+
+    def _append(self, b: bytes) -> None:
+        if self.file is None:
+            self.dest += b
+        else:
+            self.file.append(bytes(b))
+
+    def _flush(self) -> None:
+        if self.file is not None:
+            self.file.flush()
 
     def add_record(self, data: bytes) -> None:
         """log_writer.rs:58-97."""
@@ -207,7 +223,7 @@ class LogWriter:
             leftover = BLOCK_SIZE - self.block_offset
             if leftover < HEADER_SIZE:
                 if leftover > 0:
-                    self.dest += bytes(leftover)          # :66-71 zero trailer
+                    self._append(bytes(leftover))         # :66-71 zero trailer (`?`: offset kept)
                 self.block_offset = 0
             avail = BLOCK_SIZE - self.block_offset - HEADER_SIZE
             frag = left if left < avail else avail
@@ -232,9 +248,10 @@ class LogWriter:
         n = len(payload)
         assert n <= 0xFFFF
         crc = mask(extend(self.type_crc[rtype], payload))
-        self.dest += encode_fixed32(crc) + bytes([n & 0xFF, n >> 8, rtype])
-        self.dest += payload
-        self.block_offset += HEADER_SIZE + n
+        self._append(encode_fixed32(crc) + bytes([n & 0xFF, n >> 8, rtype]))  # :114
+        self._append(payload)                                                # :116
+        self._flush()                                                        # :119
+        self.block_offset += HEADER_SIZE + n                                 # :121, after every `?`
 
 
 def write_image(records: Iterable[bytes], block_offset: int = 0) -> bytes:

@@ -363,11 +363,15 @@ int emit_physical_record(revel_log_writer* w, uint8_t type, const uint8_t* data,
     hdr[1] = (uint8_t)(crc >> 8);
     hdr[2] = (uint8_t)(crc >> 16);
     hdr[3] = (uint8_t)(crc >> 24);
+    // log_writer.rs:114-121: each `?` returns before block_offset advances
     int rc = revel_writable_file_append(w->dest, hdr, REVEL_HEADER_SIZE);
-    if (rc == REVEL_OK) rc = revel_writable_file_append(w->dest, data, n);
-    if (rc == REVEL_OK) rc = revel_writable_file_flush(w->dest);  // log_writer.rs:119
+    if (rc) return rc;
+    rc = revel_writable_file_append(w->dest, data, n);
+    if (rc) return rc;
+    rc = revel_writable_file_flush(w->dest);  // log_writer.rs:119
+    if (rc) return rc;
     w->block_offset += REVEL_HEADER_SIZE + n;
-    return rc;
+    return REVEL_OK;
 }
 
 }  // namespace
@@ -563,6 +567,12 @@ struct revel_log_reader {
     bool resyncing = false;
     uint64_t last_record_offset = 0;
     std::vector<uint8_t> scratch;
+
+    // A record read_record_into could not deliver (the caller's buffer was too
+    // short): handed out by the next read call, before anything else is read.
+    const uint8_t* pending = nullptr;
+    size_t pending_n = 0;
+    bool has_pending = false;
 };
 
 namespace {
@@ -782,21 +792,60 @@ int revel_log_reader_new(revel_sequential_file* file, int checksum, uint64_t ini
     return REVEL_OK;
 }
 
-int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size_t* n) {
-    if (!r || !data || !n) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
-    *data = nullptr;
-    *n = 0;
-    r->scratch.clear();
+}  // extern "C"
+
+namespace {
+
+// Where the bytes of a logical record are assembled: the caller's buffer
+// (read_record_into) while they fit, else the reader's scratch (read_record:
+// cap 0, always the scratch).  A FULL record is not assembled: its payload is
+// handed out where it lies in the window.
+struct Assembly {
+    uint8_t* buf;
+    size_t cap;
+    size_t len = 0;
+    bool in_buf = true;
+
+    void reset(revel_log_reader* r) {
+        len = 0;
+        in_buf = true;
+        r->scratch.clear();
+    }
+    void add(revel_log_reader* r, const uint8_t* p, size_t n) {
+        if (in_buf && len + n <= cap) {
+            memcpy(buf + len, p, n);
+        } else {
+            if (in_buf) r->scratch.assign(buf, buf + len);  // spill what the caller's buffer holds
+            in_buf = false;
+            r->scratch.insert(r->scratch.end(), p, p + n);
+        }
+        len += n;
+    }
+};
+
+// log_reader.rs:76-153 (LevelDB-correct): the next logical record.  Returns
+// REVEL_OK with *eof set at the end of the file; otherwise the record is
+// either assembled in a.buf (*where == nullptr, a.len bytes) or lies at
+// *where (window or scratch, *where_n bytes).
+int next_logical(revel_log_reader* r, Assembly& a, const uint8_t** where, size_t* where_n, bool* eof) {
+    *where = nullptr;
+    *where_n = 0;
+    *eof = false;
+    a.reset(r);
     bool in_fragmented = false;
     uint64_t prospective = 0;
     for (;;) {
         if (r->rec_i >= r->recs.size()) {
-            if (r->file_eof && r->rec_i >= r->recs.size() && r->win_len == 0) return REVEL_OK;  // EOF
+            if (r->file_eof && r->rec_i >= r->recs.size() && r->win_len == 0) {  // EOF
+                *eof = true;
+                return REVEL_OK;
+            }
             int rc = load_window(r);
             if (rc) return rc;
             if (r->recs.empty()) {
                 // EOF: a partial fragmented record is dropped (log_reader.rs:133-141)
-                r->scratch.clear();
+                a.reset(r);
+                *eof = true;
                 return REVEL_OK;
             }
             continue;
@@ -812,7 +861,8 @@ int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size
                 r->recs.clear();
                 r->rec_i = 0;
                 r->win_len = 0;
-                r->scratch.clear();
+                a.reset(r);
+                *eof = true;
                 return REVEL_OK;
             }
             return set_error(REVEL_IO_ERROR, "bad record length at offset %llu", (unsigned long long)rec.file_offset);
@@ -839,23 +889,27 @@ int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size
         switch (rec.type) {
             case REVEL_FULL_TYPE:
                 r->last_record_offset = rec.file_offset;
-                *data = payload;
-                *n = rec.length;
+                a.reset(r);
+                *where = payload;
+                *where_n = rec.length;
                 return REVEL_OK;
             case REVEL_FIRST_TYPE:
                 in_fragmented = true;
                 prospective = rec.file_offset;
-                r->scratch.assign(payload, payload + rec.length);
+                a.reset(r);
+                a.add(r, payload, rec.length);
                 break;
             case REVEL_MIDDLE_TYPE:
-                if (in_fragmented) r->scratch.insert(r->scratch.end(), payload, payload + rec.length);
+                if (in_fragmented) a.add(r, payload, rec.length);
                 break;
             case REVEL_LAST_TYPE:
                 if (in_fragmented) {
-                    r->scratch.insert(r->scratch.end(), payload, payload + rec.length);
+                    a.add(r, payload, rec.length);
                     r->last_record_offset = prospective;
-                    *data = r->scratch.data();
-                    *n = r->scratch.size();
+                    if (!a.in_buf) {
+                        *where = r->scratch.data();
+                        *where_n = r->scratch.size();
+                    }
                     return REVEL_OK;
                 }
                 break;
@@ -865,6 +919,66 @@ int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size
                                  (unsigned long long)rec.file_offset);
         }
     }
+}
+
+}  // namespace
+
+extern "C" {
+
+int revel_log_reader_read_record(revel_log_reader* r, const uint8_t** data, size_t* n) {
+    if (!r || !data || !n) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
+    *data = nullptr;
+    *n = 0;
+    if (r->has_pending) {  // a record read_record_into could not deliver
+        r->has_pending = false;
+        *data = r->pending;
+        *n = r->pending_n;
+        return REVEL_OK;
+    }
+    Assembly a{nullptr, 0};  // no caller buffer: fragments go to the scratch
+    const uint8_t* where;
+    size_t wn;
+    bool eof;
+    int rc = next_logical(r, a, &where, &wn, &eof);
+    if (rc || eof) return rc;
+    *data = where;  // non-null: the window or the scratch
+    *n = wn;
+    return REVEL_OK;
+}
+
+int revel_log_reader_read_record_into(revel_log_reader* r, uint8_t* buf, size_t cap, size_t* n, int* eof) {
+    if (!r || !n || (!buf && cap)) return set_error(REVEL_INVALID_ARGUMENT, "null argument");
+    *n = 0;
+    if (eof) *eof = 0;
+    const uint8_t* where;
+    size_t wn;
+    if (r->has_pending) {
+        where = r->pending;
+        wn = r->pending_n;
+    } else {
+        Assembly a{buf, cap};
+        bool at_eof;
+        int rc = next_logical(r, a, &where, &wn, &at_eof);
+        if (rc) return rc;
+        if (at_eof) {
+            if (eof) *eof = 1;
+            return REVEL_OK;
+        }
+        if (!where) {  // assembled in the caller's buffer
+            *n = a.len;
+            return REVEL_OK;
+        }
+    }
+    *n = wn;
+    if (wn > cap) {  // keep it for the next call: the caller grows its buffer
+        r->pending = where;
+        r->pending_n = wn;
+        r->has_pending = true;
+        return set_error(REVEL_INVALID_ARGUMENT, "record of %zu bytes, buffer of %zu", wn, cap);
+    }
+    if (wn) memcpy(buf, where, wn);
+    r->has_pending = false;
+    return REVEL_OK;
 }
 
 uint64_t revel_log_reader_last_record_offset(const revel_log_reader* r) { return r ? r->last_record_offset : 0; }

@@ -19,7 +19,7 @@ import ctypes
 from ctypes import c_size_t, c_void_p
 from typing import Optional
 
-from ._lib import check, lib
+from ._lib import INVALID_ARGUMENT, check, lib
 from .env import SequentialFile, WritableFile
 
 
@@ -64,6 +64,25 @@ class Reader:
         if not p.value:
             return None
         return ctypes.string_at(p.value, n.value) if n.value else b""
+
+    def read_record_into(self, scratch: bytearray) -> Optional[memoryview]:
+        """``read_record(&mut scratch)`` with the reference's ownership
+        (log_reader.rs:76): the record is written into ``scratch``, grown
+        when the library reports the bytes it needs; returns a view of the
+        record's bytes in ``scratch``, ``None`` at EOF."""
+        n, eof = c_size_t(), ctypes.c_int()
+        while True:
+            buf = (ctypes.c_char * len(scratch)).from_buffer(scratch) if len(scratch) else None
+            rc = lib().revel_log_reader_read_record_into(self._h, buf, len(scratch), ctypes.byref(n),
+                                                         ctypes.byref(eof))
+            del buf
+            if rc == INVALID_ARGUMENT and n.value > len(scratch):
+                scratch.extend(bytes(n.value - len(scratch)))  # scratch.reserve(n), then call again
+                continue
+            check(rc)
+            if eof.value:
+                return None
+            return memoryview(scratch)[:n.value]
 
     def last_record_offset(self) -> int:
         return lib().revel_log_reader_last_record_offset(self._h)

@@ -1067,6 +1067,20 @@ def test_three_arg_reader_callbacks_every_golden(golden_index):
             assert got == want, (name, chunk)
 
 
+def test_read_record_into_gpu_verified_every_golden(golden_index):
+    """read_record_into (the caller's scratch, log_reader.rs:76) on the
+    3-argument GPU-verified reader: the same events as read_record, errors
+    included, on every golden image through caller files."""
+    from test_host_capi import reader_events
+    for name in sorted(golden_index):
+        img = golden_image(name)
+        for chunk in (1 << 30, 4096):
+            for start in (0, 64):
+                a = log.Reader(env.CallbackSequentialFile(_PySeq(img, chunk)), True, 0)
+                b = log.Reader(env.CallbackSequentialFile(_PySeq(img, chunk)), True, 0)
+                assert reader_events(a, into=bytearray(start)) == reader_events(b), (name, chunk, start)
+
+
 def test_callback_writer_then_three_arg_reader_roundtrip():
     """Writer::new(Rc<RefCell<dyn WritableFile>>) on a caller file, read back
     through Reader::new(file, true, initial_offset) with GPU verification."""

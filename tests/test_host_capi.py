@@ -153,6 +153,66 @@ def test_reader_nochecksum_all_golden(golden_index):
             assert got == want, name
 
 
+def reader_events(rd, into=None, limit=100000):
+    """Every event a Reader yields until EOF, continuing after errors (the
+    reader resumes after a bad record): record bytes, or ("error", code).
+    into = a bytearray: read through read_record_into with that scratch."""
+    out = []
+    for _ in range(limit):
+        try:
+            r = rd.read_record() if into is None else rd.read_record_into(into)
+        except RevelError as e:
+            out.append(("error", e.code))
+            continue
+        if r is None:
+            return out
+        out.append(bytes(r))
+        del r  # a view into the scratch: release it before the scratch grows
+    raise AssertionError("reader did not reach EOF")
+
+
+@pytest.mark.parametrize("start", [0, 1, 100, 1 << 20])
+def test_read_record_into_caller_scratch_every_golden(golden_index, start):
+    """read_record_into (log_reader.rs:76's `&mut Vec<u8>` scratch): the same
+    events as read_record on every golden image, whatever the scratch's size
+    to begin with (it grows by the bytes the library says it needs)."""
+    for name in sorted(golden_index):
+        img = golden_image(name)
+        for chunk in (1 << 30, 4096):
+            a = log.Reader(env.CallbackSequentialFile(PySequential(img, chunk)), checksum=False, window_bytes=65536)
+            b = log.Reader(env.CallbackSequentialFile(PySequential(img, chunk)), checksum=False, window_bytes=65536)
+            scratch = bytearray(start)
+            assert reader_events(a, into=scratch) == reader_events(b), (name, chunk, start)
+
+
+def test_read_record_into_short_buffer_keeps_the_record():
+    """A short scratch returns InvalidArgument with the bytes needed and
+    keeps the record for the next call (either read entry point)."""
+    import ctypes
+    recs = [b"x" * 10, b"y" * 70000, b"", b"z" * 5]
+    img = oc.write_image(recs)
+    rd = log.Reader(env.MemorySequentialFile(img), checksum=False, window_bytes=65536)
+    L = revel_amd.lib()
+    n, eof = ctypes.c_size_t(), ctypes.c_int()
+    buf = ctypes.create_string_buffer(16)
+    assert L.revel_log_reader_read_record_into(rd._h, buf, 16, ctypes.byref(n), ctypes.byref(eof)) == _lib.OK
+    assert (n.value, eof.value, buf.raw[:10]) == (10, 0, recs[0])
+    # the 70 000-byte record spans three blocks: too long for 16 bytes, twice
+    for _ in range(2):
+        assert L.revel_log_reader_read_record_into(rd._h, buf, 16, ctypes.byref(n), ctypes.byref(eof)) == \
+            _lib.INVALID_ARGUMENT
+        assert n.value == 70000
+    assert rd.read_record() == recs[1]  # the kept record, through the other entry point
+    assert L.revel_log_reader_read_record_into(rd._h, buf, 16, ctypes.byref(n), ctypes.byref(eof)) == _lib.OK
+    assert (n.value, eof.value) == (0, 0)  # the empty record: not EOF
+    assert L.revel_log_reader_read_record_into(rd._h, buf, 0, ctypes.byref(n), None) == _lib.INVALID_ARGUMENT
+    assert n.value == 5
+    assert L.revel_log_reader_read_record_into(rd._h, buf, 16, ctypes.byref(n), ctypes.byref(eof)) == _lib.OK
+    assert buf.raw[:5] == recs[3]
+    assert L.revel_log_reader_read_record_into(rd._h, buf, 16, ctypes.byref(n), ctypes.byref(eof)) == _lib.OK
+    assert (n.value, eof.value) == (0, 1)
+
+
 @pytest.mark.parametrize("window", [32768, 65536, 1 << 20])
 def test_reader_windows_and_fragments(window):
     rng = np.random.default_rng(5)
@@ -300,6 +360,72 @@ def test_callback_writer_shared_file_sync_and_errors():
     assert e.value.code == _lib.IO_ERROR
     wf.close()
     assert f.calls[-1] == "close"
+
+
+class ScriptedFailFile:
+    """A `dyn WritableFile` whose n-th call of one kind fails once: kind
+    "append" counts every append (trailers, headers and payloads alike),
+    "flush" every flush.  Used identically by the library's writer (through
+    callbacks) and by the oracle writer, which restates the reference's `?`
+    early returns (log_writer.rs:70, :114-121)."""
+
+    def __init__(self, kind, n):
+        self.kind, self.n = kind, n
+        self.counts = {"append": 0, "flush": 0}
+        self.data = bytearray()
+
+    def _tick(self, kind):
+        self.counts[kind] += 1
+        if kind == self.kind and self.counts[kind] == self.n:
+            raise OSError(f"{kind} #{self.n} fails")
+
+    def append(self, d):
+        self._tick("append")
+        self.data += d
+
+    def flush(self):
+        self._tick("flush")
+
+    def sync(self):
+        pass
+
+    def close(self):
+        pass
+
+
+@pytest.mark.parametrize("start", [0, 32761, 32766, 100])
+@pytest.mark.parametrize("kind,n", [("append", k) for k in range(1, 12)] + [("flush", k) for k in range(1, 6)])
+def test_writer_error_path_state_matches_reference(kind, n, start):
+    """A failed add_record leaves the bytes written before the failing call and
+    the block_offset of that point (log_writer.rs:114-121 advance it only after
+    header append, payload append and flush all succeed; a failed trailer append
+    keeps it too, :66-71); a retry then frames from there.  The failure hits
+    the trailer (start 32766: a 2-byte trailer), a header, a payload or a flush
+    of a FIRST/MIDDLE/LAST split or of FULL records."""
+    recs = [b"a" * 40000, b"b" * 10, b"", b"c" * 70000, b"d" * 5]
+    mine_f, ref_f = ScriptedFailFile(kind, n), ScriptedFailFile(kind, n)
+    w = log.Writer(env.CallbackWritableFile(mine_f), start)
+    ow = po.LogWriter(block_offset=start, file=ref_f)
+    for r in recs:
+        for attempt in range(2):  # the record that fails is retried once
+            try:
+                ow.add_record(r)
+                ref_err = None
+            except OSError as e:
+                ref_err = e
+            try:
+                w.add_record(r)
+                my_err = None
+            except RevelError as e:
+                my_err = e
+            assert (ref_err is None) == (my_err is None), (kind, n, start, r[:1], attempt)
+            if my_err is not None:
+                assert my_err.code == _lib.IO_ERROR  # io::Error -> IOError (error.rs:25-29)
+            assert w.block_offset == ow.block_offset, (kind, n, start, r[:1], attempt)
+            assert bytes(mine_f.data) == bytes(ref_f.data), (kind, n, start, r[:1], attempt)
+            if ref_err is None:
+                break
+    assert mine_f.counts == ref_f.counts
 
 
 def test_callback_writer_release_and_required_append():
