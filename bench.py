@@ -10,6 +10,14 @@ independent WAL streams, one per GPU, no collective on the data path
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`--gpus N` with N > 1 outside torch.distributed (no WORLD_SIZE) launches the N
+ranks itself: before anything touches a GPU it counts the visible gfx950
+devices (KFD topology + *_VISIBLE_DEVICES; exits non-zero when there are fewer
+than N), then runs `python -m torch.distributed.run --nproc-per-node N` on this
+script as a child process and exits with its return code.  Each rank drives
+GPU `LOCAL_RANK`; the JSON's `ranks` names every rank's device and PCI bus id
+with its own kernel time, so a record shows that N distinct GPUs ran.
+
 Prints one JSON line on rank 0.  The `cpu_baseline` leg (rank 0, N=1) times
 the oracle's bytewise table CRC -- the reference crate's algorithm class --
 on a bounded sample of the same blocks, on one host core, and checks the
@@ -18,8 +26,12 @@ GPU's CRCs for that sample against it.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,15 +40,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# The product library (and its HIP runtime) is loaded before anything else.
-from revel_amd import BLOCK_SIZE, gpu  # noqa: E402
-
+BLOCK_SIZE = 32768  # log_format.rs:26 kBlockSize
 METRIC = "CRC32C GiB/s on device-resident 32 KiB WAL blocks; % of HBM-read roofline"
 PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SEED = 0x5EED0002
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -49,7 +59,54 @@ def parse():
                     help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
-    return ap.parse_args()
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="rehearsal: allow more ranks than GPUs (rank r drives GPU r mod count)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/distributed plumbing only: no GPU work, values null (CPU tests)")
+    return ap.parse_args(argv)
+
+
+def visible_gfx950() -> int:
+    """gfx950 devices this process may use, counted WITHOUT initialising HIP
+    (the launcher must not touch the GPU before it starts the ranks): KFD
+    topology nodes with gfx_target_version 9.5.0, narrowed by the first of
+    ROCR/HIP/CUDA_VISIBLE_DEVICES that is set.  REVEL_BENCH_DEVICES overrides
+    the count (CPU tests of the launcher)."""
+    if os.environ.get("REVEL_BENCH_DEVICES"):
+        return int(os.environ["REVEL_BENCH_DEVICES"])
+    n = 0
+    for p in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
+        try:
+            with open(p) as f:
+                props = dict(line.split() for line in f if len(line.split()) == 2)
+        except OSError:
+            continue
+        if props.get("gfx_target_version") == "90500":
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
+def launch_ranks(args, argv) -> int:
+    """N ranks, one per GPU, under torch.distributed.run as a CHILD process
+    (never exec: nothing here has touched the GPU, and the child is a fresh
+    interpreter).  Rank 0's JSON line reaches stdout through the inherited
+    descriptor; the return code is the launcher's."""
+    have = visible_gfx950()
+    if args.gpus > have and not args.share_gpus and not args.dry_run:
+        print(f"bench.py: --gpus {args.gpus} but {have} gfx950 device(s) visible", file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
 
 
 class Dist:
@@ -83,6 +140,14 @@ class Dist:
         t = torch.tensor([x], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+    def gather(self, obj):
+        """Every rank's obj, in rank order (gloo all_gather_object)."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def close(self):
         if self.dist:
@@ -248,21 +313,46 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
     per = k * BLOCK_SIZE
     total = per * D.world
     d = os.environ.get("REVEL_BENCH_DIR") or tempfile.gettempdir()
-    path = os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{os.getppid() if D.world > 1 else os.getpid()}.log")
+    tag = os.environ.get("TORCHELASTIC_RUN_ID") or str(os.getppid() if D.world > 1 else os.getpid())
+    path = os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{tag}.log")
+    # every rank must see the same file on this host: a failure anywhere (no
+    # space, a write error) makes every rank skip this leg together -- the
+    # headline value is already measured and must still be printed
+    why = ""
     if D.rank == 0:
-        with open(path, "wb") as f:
-            f.truncate(total)
-    D.barrier()
+        try:
+            free = shutil.disk_usage(d).free
+            if free < total + (1 << 30):
+                why = f"{d}: {free >> 20} MiB free < {total >> 20} MiB file + 1 GiB"
+            else:
+                with open(path, "wb") as f:
+                    f.truncate(total)
+        except OSError as ex:
+            why = f"create {path}: {ex}"
+    if D.max(float(bool(why))) > 0:
+        return {"value": None, "skipped": why or "another rank could not write its part"}
+    ok = True
     host = ctx.d2h(dblocks, per)  # this rank's part of the WAL = its first k device blocks
-    fd = os.open(path, os.O_WRONLY)
     try:
-        view = memoryview(host)
-        done = 0
-        while done < per:
-            done += os.pwrite(fd, view[done:], D.rank * per + done)
-    finally:
-        os.close(fd)
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            view = memoryview(host)
+            done = 0
+            while done < per:
+                done += os.pwrite(fd, view[done:], D.rank * per + done)
+        finally:
+            os.close(fd)
+    except OSError as ex:
+        ok, why = False, f"rank {D.rank} write: {ex}"
     del host
+    if D.max(float(not ok)) > 0:
+        D.barrier()
+        if D.rank == 0:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+        return {"value": None, "skipped": why or "another rank could not write its part"}
     D.barrier()
     s, e = shard.block_ranges(total, D.world)[D.rank]
     t0 = time.perf_counter()
@@ -286,6 +376,8 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
         except OSError:
             pass
     summ = shard.Stitch(blobs).summary() if D.rank == 0 else {}
+    per_rank = D.gather({"rank": D.rank, "load_s": round(t_load, 4), "all_in_s": round(t_all, 4),
+                         "h2d_ms": round(info["h2d_ms"], 3), "verify_ms": round(info["kernel_ms"], 3)})
     return {
         "unit": "GiB/s",
         "value": round(total / 2**30 / wall_max, 2),
@@ -296,6 +388,7 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
         "h2d_GiB_s_rank0": round((e - s) / 2**30 / (info["h2d_ms"] / 1e3), 2) if info["h2d_ms"] else None,
         "read_s_rank0": round(info["read_seconds"], 3),
         "verify_ms_rank0": round(info["kernel_ms"], 3),
+        "per_rank": per_rank,
         "physical_records": summ.get("physical"),
         "bad_records": summ.get("bad"),
         "stitched": summ.get("stitched"),
@@ -337,8 +430,7 @@ def c3_records(ctx, D, gib: float, iters: int = 5):
     D.barrier()
     for _ in range(iters):
         e0.record()
-        check(L.revel_gpu_count_records(ctx.handle, img.ptr, n, counts.ptr, None))
-        check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+        check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
         check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, out.ptr, None))
         e1.record()
         ctx.sync()
@@ -365,13 +457,24 @@ def c3_records(ctx, D, gib: float, iters: int = 5):
     }
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)  # the parent never touches the GPU
     D = Dist()
+    if D.world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}", file=sys.stderr, flush=True)
+    if args.dry_run:
+        return dry_run(args, D)
+    from revel_amd import gpu  # the product library (and the HIP runtime) load here, in the ranks
     ndev = gpu.device_count()
     if ndev == 0:
         raise SystemExit("bench.py needs a gfx950 GPU (no fallback)")
-    ctx = gpu.GpuContext(D.local % ndev)  # modulo: lets ranks share one GPU when rehearsing
+    if D.world > ndev and not args.share_gpus:
+        raise SystemExit(f"bench.py: {D.world} ranks but {ndev} gfx950 device(s) visible (--share-gpus to rehearse)")
+    device = D.local % ndev  # distinct per rank unless --share-gpus
+    ctx = gpu.GpuContext(device)
     n = args.blocks
     dblocks = ctx.alloc(n * BLOCK_SIZE)
     masked = ctx.alloc(4 * n)
@@ -403,6 +506,10 @@ def main():
     wall = D.max(t1 - t0)
     kern_ms = ev0.elapsed_ms(ev1) / args.steps
     kern_ms_max = D.max(kern_ms)
+    ranks = D.gather({"rank": D.rank, "local_rank": D.local, "host": socket.gethostname(), "device": device,
+                      "pci_bus_id": gpu.pci_bus_id(device), "kernel_ms": round(kern_ms, 4),
+                      "wall_ms_per_step": round((t1 - t0) / args.steps * 1e3, 4),
+                      "all_verify_flags_ok": bool(okh.all())})
 
     total_blocks = n * D.world
     value = total_blocks * BLOCK_SIZE / 2**30 / (wall / args.steps)
@@ -423,46 +530,70 @@ def main():
         cpu = cpu_baseline(ctx, dblocks, masked, n, args.cpu_seconds)
 
     if D.rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": round(value, 1),
-            "unit": "GiB/s",
-            "n_gpus": D.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic: splitmix64 payloads generated + framed (masked CRC headers) on device",
-            "config": {
-                "workload": "C2: device-resident full-type 32 KiB WAL blocks, masked CRC32C(type||payload) "
-                            "compute + verify vs stored header, one wavefront per block",
-                "blocks_per_gpu": n,
-                "bytes_per_gpu": n * BLOCK_SIZE,
-                "parallelism": f"independent WAL stream per GPU x{D.world} (no collective)",
-                "kernel_variant": "production" if args.variant is None else args.variant,
-                "all_verify_flags_ok": all_ok,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_source,
-                "kernel_ms": round(kern_ms_max, 4),
-                "alg_bytes_per_launch": alg_bytes,
-            },
-            "cpu_baseline": cpu,
-            "end_to_end": e2e,
-            "c3": c3,
+        out = result_line(args, D, ranks, value=round(value, 1), ms=round(wall / args.steps * 1e3, 4))
+        out["config"].update({"kernel_variant": "production" if args.variant is None else args.variant,
+                              "all_verify_flags_ok": all_ok})
+        out["roofline"] = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_source,
+            "kernel_ms": round(kern_ms_max, 4),
+            "alg_bytes_per_launch": alg_bytes,
         }
+        out["cpu_baseline"] = cpu
+        out["end_to_end"] = e2e
+        out["c3"] = c3
         print(json.dumps(out), flush=True)
     D.close()
+    return 0
+
+
+def result_line(args, D, ranks, value, ms):
+    """The JSON line's contract fields (values filled by the caller)."""
+    n = args.blocks
+    distinct = len({(r["host"], r["pci_bus_id"]) for r in ranks})
+    return {
+        "metric": METRIC,
+        "value": value,
+        "unit": "GiB/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: splitmix64 payloads generated + framed (masked CRC headers) on device",
+        "config": {
+            "workload": "C2: device-resident full-type 32 KiB WAL blocks, masked CRC32C(type||payload) "
+                        "compute + verify vs stored header, one wavefront per block",
+            "blocks_per_gpu": n,
+            "bytes_per_gpu": n * BLOCK_SIZE,
+            "parallelism": f"independent WAL stream per GPU x{D.world} (no collective)",
+            "distinct_devices": distinct,
+        },
+        "ranks": ranks,
+    }
+
+
+def dry_run(args, D):
+    """The launcher and the distributed plumbing without a GPU: every rank
+    reports itself, rank 0 prints the line with null values."""
+    D.barrier()
+    ranks = D.gather({"rank": D.rank, "local_rank": D.local, "host": socket.gethostname(), "device": D.local,
+                      "pci_bus_id": f"dry-run-{D.local}", "kernel_ms": None})
+    if D.rank == 0:
+        out = result_line(args, D, ranks, value=None, ms=None)
+        out["dry_run"] = True
+        print(json.dumps(out), flush=True)
+    D.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -141,6 +141,9 @@ void revel_log_writer_free(revel_log_writer* w);
 typedef struct revel_gpu_context revel_gpu_context;
 /* Number of visible gfx950 devices (0 on a host without one). */
 int revel_gpu_device_count(int* count);
+/* PCI bus id ("dddd:bb:dd.f") of a visible HIP device: which physical GPU a
+ * process drove (bench.py reports it per rank). */
+int revel_gpu_device_pci_bus_id(int device, char* buf, size_t cap);
 /* One context per (thread, device): owns a HIP stream and scratch.  Every
  * GPU entry point binds the context's device for the duration of the call and
  * restores the calling thread's current device before it returns. */
@@ -231,19 +234,21 @@ int revel_gpu_frame_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t n
  * output:  (1) count physical records of each block of the image
  * (d_counts[nblocks]); (2) walk + CRC every record, writing record k of
  * block b to d_out[d_first[b] + k] where d_first is the exclusive prefix sum
- * of d_counts (revel_gpu_exclusive_scan_u32 computes it on device).
+ * of d_counts (revel_gpu_exclusive_scan_u32 computes it on device;
+ * revel_gpu_count_scan_records does the count and the scan in one call, the
+ * scan taking the count pass's per-64-block sums as its first pass).
  * nbytes need not be a block multiple (the last block may be partial).
  * The count pass also leaves per-block header lists in the context: a verify
  * of the same image on the same context uses them (for blocks with more than
- * 64 records it first lists the rest into their own d_out slots, which it
+ * 256 records it first lists the rest into their own d_out slots, which it
  * then overwrites with the results); without them verify walks the headers
- * itself, with the same results, slower.  It also leaves the records per 64
- * blocks: the next revel_gpu_exclusive_scan_u32 of exactly that d_counts array
- * and n = its block count, before anything writes d_counts, uses them as its
- * first pass (one launch instead of two); any other scan takes the general
- * path. */
+ * itself, with the same results, slower.  A context's count -> verify pair
+ * must not interleave with another on that context (use one context per
+ * concurrent stream). */
 int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,
                             uint32_t* d_counts, void* stream);
+int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,
+                                 uint32_t* d_counts, uint32_t* d_first, void* stream);
 int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, uint32_t* d_out,
                                  size_t n, void* stream);
 int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes,

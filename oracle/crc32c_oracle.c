@@ -179,9 +179,10 @@ size_t oracle_write_image(const uint8_t* payloads, const uint64_t* lens, size_t 
 
 /* Physical-record walk (same rules as walk_block() in crc32c_oracle.py).
  * Writes up to `cap` records; returns the number found (may exceed cap). */
-size_t oracle_walk(const uint8_t* image, size_t n, uint64_t* rec_off, uint32_t* rec_len,
-                   uint8_t* rec_type, uint32_t* rec_stored, uint32_t* rec_computed,
-                   uint8_t* rec_status, size_t cap) {
+size_t oracle_walk_v(const uint8_t* image, size_t n, uint64_t* rec_off, uint32_t* rec_len,
+                     uint8_t* rec_type, uint32_t* rec_stored, uint32_t* rec_computed,
+                     uint8_t* rec_status, size_t cap, int variant) {
+    const crc_fn crc = pick(variant);
     size_t count = 0;
     for (size_t base = 0; base < n; base += ORACLE_BLOCK) {
         size_t bl = n - base < ORACLE_BLOCK ? n - base : ORACLE_BLOCK;
@@ -197,7 +198,8 @@ size_t oracle_walk(const uint8_t* image, size_t n, uint64_t* rec_off, uint32_t* 
             if (ORACLE_HEADER + len > bl - off) { status = 2; stop = 1; }
             else if (type == 0 && len == 0) { status = 3; stop = 1; }
             else {
-                computed = oracle_mask(oracle_value(h + 6, len + 1));
+                /* log_writer.rs:107-111: mask(crc of type || payload) */
+                computed = oracle_mask(crc(0xFFFFFFFFu, h + 6, len + 1) ^ 0xFFFFFFFFu);
                 status = computed == stored ? 0 : 1;
             }
             if (count < cap) {
@@ -210,6 +212,12 @@ size_t oracle_walk(const uint8_t* image, size_t n, uint64_t* rec_off, uint32_t* 
         }
     }
     return count;
+}
+
+size_t oracle_walk(const uint8_t* image, size_t n, uint64_t* rec_off, uint32_t* rec_len,
+                   uint8_t* rec_type, uint32_t* rec_stored, uint32_t* rec_computed,
+                   uint8_t* rec_status, size_t cap) {
+    return oracle_walk_v(image, n, rec_off, rec_len, rec_type, rec_stored, rec_computed, rec_status, cap, 0);
 }
 
 /* Config C2 generator (identical bytes to synth_full_blocks() in Python and

@@ -41,6 +41,8 @@ def lib():
         L.oracle_write_image.argtypes = [c_void_p, c_void_p, c_size_t, POINTER(c_uint64), c_void_p, c_size_t]
         L.oracle_walk.restype = c_size_t
         L.oracle_walk.argtypes = [c_void_p, c_size_t] + [c_void_p] * 6 + [c_size_t]
+        L.oracle_walk_v.restype = c_size_t
+        L.oracle_walk_v.argtypes = [c_void_p, c_size_t] + [c_void_p] * 6 + [c_size_t, c_int]
         L.oracle_synth_full_blocks.restype = None
         L.oracle_synth_full_blocks.argtypes = [c_void_p, c_size_t, c_uint64, c_uint64]
         _lib = L
@@ -84,15 +86,23 @@ WALK_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("type", "u1")
                        ("computed_crc", "<u4"), ("status", "u1")])
 
 
-def walk(image: bytes) -> np.ndarray:
-    """Every physical record: file_offset, length, type, stored, computed, status."""
-    img = np.frombuffer(image, dtype=np.uint8) if image else np.zeros(1, np.uint8)
-    n = len(image)
+def walk(image, variant: str = "bytewise") -> np.ndarray:
+    """Every physical record: file_offset, length, type, stored, computed, status.
+    image: bytes or a uint8 array; variant: the CRC implementation (bytewise =
+    the reference crate's algorithm class; sse42 for GiB-sized images)."""
+    if isinstance(image, np.ndarray):
+        img = np.ascontiguousarray(image, dtype=np.uint8).ravel()
+        n = img.size
+    else:
+        n = len(image)
+        img = np.frombuffer(image, dtype=np.uint8) if image else None
+    if n == 0:
+        img = np.zeros(1, np.uint8)
     cap = max(1, n // 7 + 8)
     off = np.empty(cap, np.uint64); ln = np.empty(cap, np.uint32); ty = np.empty(cap, np.uint8)
     st = np.empty(cap, np.uint32); co = np.empty(cap, np.uint32); ss = np.empty(cap, np.uint8)
-    k = lib().oracle_walk(img.ctypes.data, n, off.ctypes.data, ln.ctypes.data, ty.ctypes.data,
-                          st.ctypes.data, co.ctypes.data, ss.ctypes.data, cap)
+    k = lib().oracle_walk_v(img.ctypes.data, n, off.ctypes.data, ln.ctypes.data, ty.ctypes.data,
+                            st.ctypes.data, co.ctypes.data, ss.ctypes.data, cap, VARIANTS[variant])
     assert k <= cap
     out = np.empty(k, dtype=WALK_DTYPE)
     out["file_offset"], out["length"], out["type"] = off[:k], ln[:k], ty[:k]

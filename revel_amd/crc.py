@@ -4,10 +4,6 @@ from __future__ import annotations
 from ._lib import lib
 
 
-def _buf(data: bytes):
-    return (data, len(data))
-
-
 def value(data: bytes) -> int:
     """crc.rs:17-19 ``value(data)``."""
     return lib().revel_crc32c_value(data, len(data))

@@ -161,6 +161,21 @@ int revel_gpu_device_count(int* count) {
     return REVEL_OK;
 }
 
+int revel_gpu_device_pci_bus_id(int device, char* buf, size_t cap) {
+    if (!buf || cap == 0) return set_error(REVEL_INVALID_ARGUMENT, "null buffer");
+    buf[0] = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        (void)hipGetLastError();
+        return set_error(REVEL_INVALID_ARGUMENT, "device %d not visible", device);
+    }
+    char id[64] = {0};
+    HIP_TRY(hipDeviceGetPCIBusId(id, (int)sizeof id, device), "hipDeviceGetPCIBusId");
+    if (strlen(id) + 1 > cap) return set_error(REVEL_INVALID_ARGUMENT, "buffer of %zu bytes < %zu", cap, strlen(id) + 1);
+    memcpy(buf, id, strlen(id) + 1);
+    return REVEL_OK;
+}
+
 int revel_gpu_context_new(int device, revel_gpu_context** out) {
     if (!out) return set_error(REVEL_INVALID_ARGUMENT, "null out");
     *out = nullptr;
@@ -200,14 +215,21 @@ void revel_gpu_context_free(revel_gpu_context* ctx) {
 
 int revel_gpu_context_trim(revel_gpu_context* ctx) {
     CHECK_CTX(ctx);
+    // free everything, forget it, then report the first failure: a buffer is
+    // never left recorded after it was freed (destroy_context would free it again)
     auto& pr = ctx->parked_reader;
-    if (pr.h_win) HIP_TRY(hipHostFree(pr.h_win), "hipHostFree");
-    if (pr.d_win) HIP_TRY(hipFree(pr.d_win), "hipFree");
-    if (pr.d_counts) HIP_TRY(hipFree(pr.d_counts), "hipFree");
-    if (pr.d_first) HIP_TRY(hipFree(pr.d_first), "hipFree");
-    if (pr.d_out) HIP_TRY(hipFree(pr.d_out), "hipFree");
+    hipError_t first = hipSuccess;
+    auto note = [&](hipError_t e) {
+        if (first == hipSuccess) first = e;
+    };
+    if (pr.h_win) note(hipHostFree(pr.h_win));
+    if (pr.d_win) note(hipFree(pr.d_win));
+    if (pr.d_counts) note(hipFree(pr.d_counts));
+    if (pr.d_first) note(hipFree(pr.d_first));
+    if (pr.d_out) note(hipFree(pr.d_out));
     pr = revel_gpu_context::ParkedReader{};
     revel::free_shard_ring(ctx);
+    if (first != hipSuccess) return hip_fail(first, "revel_gpu_context_trim");
     return REVEL_OK;
 }
 
@@ -240,11 +262,12 @@ int revel_gpu_synth_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t n
     return REVEL_OK;
 }
 
-int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts,
-                            void* stream) {
-    CHECK_CTX(ctx);
-    if (nbytes == 0) return REVEL_OK;
-    if (!d_image || !d_counts) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+namespace {
+// The count pass of revel_gpu_count_records / revel_gpu_count_scan_records:
+// counts + header lists (ctx->hlist, for the next verify of this image) and,
+// with wsums, the records per 64 blocks (the scan's first pass).
+int count_pass(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts, hipStream_t st,
+               bool wsums) {
     const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     if (nblocks > ctx->hlist_cap_blocks) {
         if (ctx->hlist) (void)hipFree(ctx->hlist);
@@ -254,21 +277,45 @@ int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t 
                 "hipMalloc(header list)");
         ctx->hlist_cap_blocks = nblocks;
     }
-    const uint64_t nw = revel::count_wave_sums(nblocks);
-    if (nw > ctx->wsums_cap) {
-        if (ctx->wsums) (void)hipFree(ctx->wsums);
-        ctx->wsums = nullptr;
-        ctx->wsums_cap = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->wsums), nw * sizeof(uint32_t)), "hipMalloc(wave sums)");
-        ctx->wsums_cap = nw;
+    if (wsums) {
+        const uint64_t nw = revel::count_wave_sums(nblocks);
+        if (nw > ctx->wsums_cap) {
+            if (ctx->wsums) (void)hipFree(ctx->wsums);
+            ctx->wsums = nullptr;
+            ctx->wsums_cap = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->wsums), nw * sizeof(uint32_t)), "hipMalloc(wave sums)");
+            ctx->wsums_cap = nw;
+        }
     }
-    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, ctx->hlist, pick(ctx, stream), ctx->wsums),
+    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, ctx->hlist, st, wsums ? ctx->wsums : nullptr),
             "count_records launch");
-    ctx->wsums_counts = d_counts;
-    ctx->wsums_n = nblocks;
     ctx->hlist_image = d_image;
     ctx->hlist_nbytes = nbytes;
     ctx->hlist_counts = d_counts;
+    return REVEL_OK;
+}
+}  // namespace
+
+int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts,
+                            void* stream) {
+    CHECK_CTX(ctx);
+    if (nbytes == 0) return REVEL_OK;
+    if (!d_image || !d_counts) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    return count_pass(ctx, d_image, nbytes, d_counts, pick(ctx, stream), false);
+}
+
+int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts,
+                                 uint32_t* d_first, void* stream) {
+    CHECK_CTX(ctx);
+    if (nbytes == 0) return REVEL_OK;
+    if (!d_image || !d_counts || !d_first) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
+    const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
+    hipStream_t st = pick(ctx, stream);
+    int rc = count_pass(ctx, d_image, nbytes, d_counts, st, true);
+    if (rc) return rc;
+    // the count pass's records per 64 blocks are the scan's first pass (one
+    // launch instead of two); they are read on the same stream right after
+    HIP_TRY(revel::exclusive_scan_counts(ctx->di, d_counts, d_first, nblocks, ctx->wsums, st), "scan launch");
     return REVEL_OK;
 }
 
@@ -277,13 +324,6 @@ int revel_gpu_exclusive_scan_u32(revel_gpu_context* ctx, const uint32_t* d_in, u
     CHECK_CTX(ctx);
     if (n == 0) return REVEL_OK;
     if (!d_in || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    if (ctx->wsums_counts == d_in && ctx->wsums_n == n) {
-        // the counts of the last count pass: its per-64-block sums are the
-        // scan's first pass (one launch instead of two)
-        ctx->wsums_counts = nullptr;
-        HIP_TRY(revel::exclusive_scan_counts(ctx->di, d_in, d_out, n, ctx->wsums, pick(ctx, stream)), "scan launch");
-        return REVEL_OK;
-    }
     const uint64_t words = revel::scan_scratch_words(n);
     if (words > ctx->scan_scratch_cap) {
         if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);

@@ -233,8 +233,6 @@ struct revel_gpu_context {
     // consumed by the next revel_gpu_exclusive_scan_u32 of exactly those counts
     uint32_t* wsums = nullptr;
     uint64_t wsums_cap = 0;
-    const uint32_t* wsums_counts = nullptr;  // the counts they sum (nullptr: none pending)
-    uint64_t wsums_n = 0;
     revel::ScratchArena arena;  // per-call scratch of decode_batches / reassemble / append framing
     // Window buffers of the last revel_log_reader freed on this context, parked
     // for the next reader with the same window (host_log.cpp): a reader per log

@@ -624,8 +624,7 @@ int gpu_verify_window(revel_log_reader* r) {
     void* st = revel_gpu_context_stream(g);
     const size_t nblocks = (r->win_len + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     int rc = revel_gpu_memcpy_h2d(g, r->d_win, r->win, r->win_len, st);
-    if (!rc) rc = revel_gpu_count_records(g, r->d_win, r->win_len, r->d_counts, st);
-    if (!rc) rc = revel_gpu_exclusive_scan_u32(g, r->d_counts, r->d_first, nblocks, st);
+    if (!rc) rc = revel_gpu_count_scan_records(g, r->d_win, r->win_len, r->d_counts, r->d_first, st);
     uint32_t tail[2] = {0, 0};
     if (!rc) rc = revel_gpu_memcpy_d2h(g, &tail[0], r->d_first + (nblocks - 1), 4, st);
     if (!rc) rc = revel_gpu_memcpy_d2h(g, &tail[1], r->d_counts + (nblocks - 1), 4, st);

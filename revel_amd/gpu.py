@@ -34,6 +34,13 @@ def device_count() -> int:
     return n.value
 
 
+def pci_bus_id(device: int) -> str:
+    """PCI bus id of a visible HIP device (which physical GPU ran)."""
+    buf = ctypes.create_string_buffer(64)
+    check(lib().revel_gpu_device_pci_bus_id(device, buf, 64))
+    return buf.value.decode()
+
+
 class DeviceBuffer:
     def __init__(self, ctx: "GpuContext", nbytes: int):
         self.ctx = ctx
@@ -186,8 +193,7 @@ class GpuContext:
         counts = self.alloc(4 * nblocks)
         first = self.alloc(4 * nblocks)
         L = lib()
-        check(L.revel_gpu_count_records(self._h, image.ptr, nbytes, counts.ptr, None))
-        check(L.revel_gpu_exclusive_scan_u32(self._h, counts.ptr, first.ptr, nblocks, None))
+        check(L.revel_gpu_count_scan_records(self._h, image.ptr, nbytes, counts.ptr, first.ptr, None))
         tail_first = self.d2h(first, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         tail_count = self.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         total = int(tail_first) + int(tail_count)

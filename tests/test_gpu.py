@@ -604,11 +604,13 @@ def test_exclusive_scan(gpu_ctx, n):
 
 
 @pytest.mark.parametrize("nblocks", [1, 63, 64, 65, 1023, 1024, 1025, 4100])
-def test_scan_of_counts_after_count_pass(gpu_ctx, nblocks):
-    """The scan right after a count pass of the same counts uses the count
-    pass's per-64-block sums (one launch); a second scan of them, a scan of a
-    prefix, and a scan after another count pass take the general path.  All
-    equal the oracle walk's per-block record counts scanned on the host."""
+def test_count_scan_records_and_general_scan(gpu_ctx, nblocks):
+    """revel_gpu_count_scan_records (count + a scan whose first pass is the
+    count pass's per-64-block sums) and the general revel_gpu_exclusive_scan_u32
+    of the same counts, of a prefix of them, and of a counts buffer freed and
+    reallocated (same size: a caching allocator hands back the same address)
+    holding other data: all equal the oracle walk's counts scanned on the host.
+    The general scan never takes the count pass's sums."""
     from revel_amd._lib import check, lib
     L = lib()
     rng = np.random.default_rng(nblocks)
@@ -622,19 +624,27 @@ def test_scan_of_counts_after_count_pass(gpu_ctx, nblocks):
     want = np.concatenate([[0], np.cumsum(want_counts, dtype=np.uint64)[:-1]]).astype(np.uint32)
     d = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
     counts, first, first2 = gpu_ctx.alloc(4 * nb), gpu_ctx.alloc(4 * nb), gpu_ctx.alloc(4 * nb)
-    check(L.revel_gpu_count_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, None))
-    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first.ptr, nb, None))   # one launch
-    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first2.ptr, nb, None))  # general
+    check(L.revel_gpu_count_scan_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, first.ptr, None))
+    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first2.ptr, nb, None))
     gpu_ctx.sync()
     assert np.array_equal(gpu_ctx.d2h(counts, 4 * nb, np.uint32), want_counts)
     assert np.array_equal(gpu_ctx.d2h(first, 4 * nb, np.uint32), want)
     assert np.array_equal(gpu_ctx.d2h(first2, 4 * nb, np.uint32), want)
-    # a prefix of the counts right after a count pass: general path
-    check(L.revel_gpu_count_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, None))
     k = max(1, nb // 2)
+    check(L.revel_gpu_count_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, None))
     check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts.ptr, first2.ptr, k, None))
     gpu_ctx.sync()
     assert np.array_equal(gpu_ctx.d2h(first2, 4 * k, np.uint32), want[:k])
+    # count pass, free its counts, new counts buffer of the same size with other data, scan it
+    check(L.revel_gpu_count_records(gpu_ctx.handle, d.ptr, len(img), counts.ptr, None))
+    gpu_ctx.sync()
+    counts.free()
+    other = rng.integers(0, 4682, nb, dtype=np.uint32)
+    counts2 = gpu_ctx.upload(other)
+    check(L.revel_gpu_exclusive_scan_u32(gpu_ctx.handle, counts2.ptr, first2.ptr, nb, None))
+    gpu_ctx.sync()
+    want2 = np.concatenate([[0], np.cumsum(other, dtype=np.uint64)[:-1]]).astype(np.uint32)
+    assert np.array_equal(gpu_ctx.d2h(first2, 4 * nb, np.uint32), want2)
 
 
 # ---- device replay reassembly vs the oracle reader's event sequence ----

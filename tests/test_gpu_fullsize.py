@@ -6,8 +6,11 @@ properties (the oracle checks every value where it can in seconds):
   bytewise one on a sample) over the whole 32 GiB, then 257 blocks corrupted
   -> exactly those flagged;
 * C3: a 1 GiB Zipf image framed on the device (revel_gpu_append_records),
-  verified: every record OK, record count = the host fragment layout,
-  computed == stored; 1 000 payload bit flips -> exactly those records flagged;
+  verified: every record's offset, length, type, stored and computed CRC and
+  status equal to the C oracle's walk of the same bytes copied back (SSE4.2
+  over the whole GiB, bytewise on the first 16 MiB), record count = the host
+  fragment layout; 1 000 payload bit flips -> exactly those records flagged and
+  the oracle walk of the flipped bytes equal again;
 * one WAL across 3 contexts at 256 MiB: the sharded replay's stream equals the
   oracle Reader's, and its counts equal the whole-image verify's."""
 import numpy as np
@@ -68,18 +71,37 @@ def test_c3_full_size_append_verify_roundtrip(gpu_ctx):
     res = gpu_ctx.verify_image(img, n)
     assert len(res) == nfrag
     assert (res["status"] == 0).all()
-    assert np.array_equal(res["computed_crc"], res["stored_crc"])
     assert int(res["length"].astype(np.uint64).sum()) == int(sizes.sum())
-    # 1 000 payload bit flips -> exactly those records flagged
+    # every record against the C oracle's walk of the same 1 GiB (SSE4.2 CRC:
+    # seconds; the bytewise table CRC -- the reference crate's algorithm class --
+    # on the first 16 MiB)
+    host = gpu_ctx.d2h(img, n)
+    assert_walk_equal(res, oc.walk(host, "sse42"))
+    head = 512 * BLOCK_SIZE
+    assert_walk_equal(res[res["file_offset"] < head], oc.walk(host[:head], "bytewise"))
+    # 1 000 payload bit flips -> exactly those records flagged, every field
+    # again equal to the oracle's walk of the flipped image
     cand = np.flatnonzero(res["length"] > 0)
     victims = np.sort(rng.choice(cand, 1000, replace=False))
     for v in victims:
         off = int(res["file_offset"][v]) + 7 + int(rng.integers(0, int(res["length"][v])))
         byte = gpu_ctx.d2h(img, 1, src_offset=off)
         gpu_ctx.h2d(img, byte ^ np.uint8(0x20), dst_offset=off)
+        host[off] ^= np.uint8(0x20)
     res2 = gpu_ctx.verify_image(img, n)
     assert np.array_equal(np.flatnonzero(res2["status"] != 0), victims)
     assert (res2["status"][victims] == 1).all()
+    assert np.array_equal(gpu_ctx.d2h(img, n), host)
+    assert_walk_equal(res2, oc.walk(host, "sse42"))
+
+
+def assert_walk_equal(res, ref):
+    """GPU verify results == the oracle walk, field by field (computed CRC
+    only where the record's length is valid: the oracle leaves it 0 as the
+    kernels do)."""
+    assert len(res) == len(ref)
+    for f in ("file_offset", "length", "type", "stored_crc", "computed_crc", "status"):
+        assert np.array_equal(res[f], ref[f].astype(res[f].dtype)), f
 
 
 def po_framed_size(sizes):

@@ -70,3 +70,35 @@ def test_sharded_walk_and_stitch_gloo(world):
     assert summ["records"] == len(recs) and summ["errors"] == 0 and summ["stitched"] >= 1
     assert summ["payload_bytes"] == sum(len(r) for r in recs)
     assert mx == float(world) and sm == float(world)
+
+
+def _bench(args, devices, timeout=240):
+    import subprocess
+    import sys
+    env = dict(os.environ, REVEL_BENCH_DEVICES=str(devices))
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` outside torch.distributed starts the 2 ranks itself
+    (torch.distributed.run as a child process, gloo) and rank 0 prints one JSON
+    line with n_gpus 2 and one `ranks` entry per rank (stub device count, no
+    GPU work: --dry-run)."""
+    import json
+    p = _bench(["--gpus", "2", "--dry-run", "--blocks", "64"], devices=2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"]
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    assert [r["device"] for r in d["ranks"]] == [0, 1]
+    assert d["config"]["distinct_devices"] == 2
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    p = _bench(["--gpus", "4", "--blocks", "64"], devices=2, timeout=60)
+    assert p.returncode == 2
+    assert "2 gfx950 device(s) visible" in p.stderr

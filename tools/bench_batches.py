@@ -52,8 +52,7 @@ def run(ctx, name, per_batch, target, iters):
     nblocks = (n + 32767) // 32768
     counts, first = ctx.alloc(4 * nblocks), ctx.alloc(4 * nblocks)
     # physical record count: run once
-    check(L.revel_gpu_count_records(ctx.handle, img.ptr, n, counts.ptr, None))
-    check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+    check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
     ctx.sync()
     nphys = int(ctx.d2h(first, 4 * nblocks, np.uint32)[-1]) + int(ctx.d2h(counts, 4 * nblocks, np.uint32)[-1])
     phys = ctx.alloc(nphys * RECORD_DTYPE.itemsize)
@@ -67,8 +66,7 @@ def run(ctx, name, per_batch, target, iters):
     t = {"verify": [], "reassemble": [], "decode": [], "total": []}
     for _ in range(iters):
         ev[0].record()
-        check(L.revel_gpu_count_records(ctx.handle, img.ptr, n, counts.ptr, None))
-        check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+        check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
         check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, phys.ptr, None))
         ev[1].record()
         check(L.revel_gpu_reassemble(ctx.handle, img.ptr, 0, n, phys.ptr, nphys, 1, logical.ptr, payload.ptr,

@@ -92,8 +92,7 @@ def main():
 
     def run(variant):
         e0.record()
-        check(L.revel_gpu_count_records(ctx.handle, d.ptr, n, counts.ptr, None))
-        check(L.revel_gpu_exclusive_scan_u32(ctx.handle, counts.ptr, first.ptr, nblocks, None))
+        check(L.revel_gpu_count_scan_records(ctx.handle, d.ptr, n, counts.ptr, first.ptr, None))
         e1.record()
         if variant == 0:  # production, from the product library
             check(L.revel_gpu_verify_records(ctx.handle, d.ptr, n, 0, first.ptr, out.ptr, None))
