@@ -4,7 +4,7 @@
 set -u
 tag=$1; A=$2; B=$3; n=${4:-3}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/ab_$tag
+O=$R/gpurun_out/$tag/ab
 mkdir -p "$O"
 for i in $(seq 1 "$n"); do
   for L in "$A" "$B"; do
