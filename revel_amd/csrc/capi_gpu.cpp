@@ -263,11 +263,11 @@ int revel_gpu_synth_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t n
 }
 
 namespace {
-// The count pass of revel_gpu_count_records / revel_gpu_count_scan_records:
-// counts + header lists (ctx->hlist, for the next verify of this image) and,
-// with wsums, the records per 64 blocks (the scan's first pass).
-int count_pass(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts, hipStream_t st,
-               bool wsums) {
+// The count pass of revel_gpu_count_records / revel_gpu_count_scan_records
+// (k_count_hist): counts, the header lists (ctx->hlist, for the next verify of
+// this image), the records per 64 blocks (ctx->wsums, the scan's first pass)
+// and the block order's histogram rows (in the block-list area after the lists).
+int count_pass(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts, hipStream_t st) {
     const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     if (nblocks > ctx->hlist_cap_blocks) {
         if (ctx->hlist) (void)hipFree(ctx->hlist);
@@ -277,21 +277,21 @@ int count_pass(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint3
                 "hipMalloc(header list)");
         ctx->hlist_cap_blocks = nblocks;
     }
-    if (wsums) {
-        const uint64_t nw = revel::count_wave_sums(nblocks);
-        if (nw > ctx->wsums_cap) {
-            if (ctx->wsums) (void)hipFree(ctx->wsums);
-            ctx->wsums = nullptr;
-            ctx->wsums_cap = 0;
-            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->wsums), nw * sizeof(uint32_t)), "hipMalloc(wave sums)");
-            ctx->wsums_cap = nw;
-        }
+    const uint64_t nw = revel::count_wave_sums(nblocks);
+    if (nw > ctx->wsums_cap) {
+        if (ctx->wsums) (void)hipFree(ctx->wsums);
+        ctx->wsums = nullptr;
+        ctx->wsums_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->wsums), nw * sizeof(uint32_t)), "hipMalloc(wave sums)");
+        ctx->wsums_cap = nw;
     }
-    HIP_TRY(revel::count_records(ctx->di, d_image, nbytes, d_counts, ctx->hlist, st, wsums ? ctx->wsums : nullptr),
+    HIP_TRY(revel::count_hist(ctx->di, d_image, nbytes, d_counts, ctx->hlist, ctx->wsums,
+                              revel::block_list_of(ctx->hlist, nblocks), st),
             "count_records launch");
     ctx->hlist_image = d_image;
     ctx->hlist_nbytes = nbytes;
     ctx->hlist_counts = d_counts;
+    ctx->hlist_list_ready = false;
     return REVEL_OK;
 }
 }  // namespace
@@ -301,7 +301,7 @@ int revel_gpu_count_records(revel_gpu_context* ctx, const void* d_image, size_t 
     CHECK_CTX(ctx);
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_counts) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
-    return count_pass(ctx, d_image, nbytes, d_counts, pick(ctx, stream), false);
+    return count_pass(ctx, d_image, nbytes, d_counts, pick(ctx, stream));
 }
 
 int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts,
@@ -311,11 +311,14 @@ int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, si
     if (!d_image || !d_counts || !d_first) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     hipStream_t st = pick(ctx, stream);
-    int rc = count_pass(ctx, d_image, nbytes, d_counts, st, true);
+    int rc = count_pass(ctx, d_image, nbytes, d_counts, st);
     if (rc) return rc;
-    // the count pass's records per 64 blocks are the scan's first pass (one
-    // launch instead of two); they are read on the same stream right after
-    HIP_TRY(revel::exclusive_scan_counts(ctx->di, d_counts, d_first, nblocks, ctx->wsums, st), "scan launch");
+    // one launch for the scan (first pass: the count pass's per-64-block sums)
+    // and verify's block list (from the count pass's histogram rows)
+    HIP_TRY(revel::scan_order(ctx->di, nbytes, d_counts, ctx->wsums, d_first, revel::block_list_of(ctx->hlist, nblocks),
+                              st),
+            "scan launch");
+    ctx->hlist_list_ready = true;
     return REVEL_OK;
 }
 
@@ -343,7 +346,8 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
     HIP_TRY(revel::verify_records(ctx->di, d_image, nbytes, base_offset, d_first, d_out, memo ? ctx->hlist : nullptr,
-                                  memo ? ctx->hlist_counts : nullptr, pick(ctx, stream)),
+                                  memo ? ctx->hlist_counts : nullptr, pick(ctx, stream),
+                                  memo && ctx->hlist_list_ready),
             "verify_records launch");
     ctx->hlist_image = nullptr;  // one count pass -> one verify
     return REVEL_OK;

@@ -10,19 +10,32 @@
 //   log_reader.rs:200-206  unmask(stored) == value(type||payload) (reader side)
 //   util/crc.rs:13-44      CRC_32_ISCSI + mask/unmask
 //
-// Work decomposition: ONE WAVEFRONT PER 32 KiB LOG BLOCK.  Lane i owns the
-// contiguous 512-byte chunk [512 i, 512 i + 512) of its block and runs a
-// table-driven CRC over it from a zero register; the 64 partial registers are
-// then combined by a wavefront GF(2) polynomial-shift reduction:
-//     R(block) = XOR_i  R_i * x^(8*512*(63-i))  mod P
-// (each lane multiplies by its own constant, then an xor-butterfly across the
-// wave).  Init/xorout enter once per record as a length-dependent constant.
-// No MFMA: this is GF(2) arithmetic, not a contraction.
+// Work decomposition: ONE WAVEFRONT PER 32 KiB LOG BLOCK, read as 32 coalesced
+// 1 KiB rows (lane i loads the 16 B at 1024 g + 16 i of row g, through a
+// register ring of rows in flight).
+//  * C2 (k_full_blocks4, k_blocks.hip): INTERLEAVED WORD STREAMS.  Stream s
+//    (0..255) is the 32-bit words at 4 s + 1024 g; lane i owns streams
+//    4i..4i+3 (the four words of its 16-B load), four independent CRC chains.
+//    Consecutive words of a stream are 1024 B apart, so the slice-by-4 tables
+//    are premultiplied by x^(8*1020) (GAP-FOLDED TABLES, GapTables below): one
+//    table step absorbs a word AND the 1020 bytes of other streams after it.
+//    At the block end the 256 stream registers are combined by an
+//    INVERSE-SHIFT TREE: R = XOR_s U_s * x^(-32 s) mod P, 8 levels of 4 table
+//    lookups (2 in-lane, 6 across lanes; x is invertible mod P since P(0) = 1).
+//  * C3 (k_verify_rows, verify_rows.inc): the same rows, transposed by
+//    permlane swaps so lane i owns ONE 4-byte column of each 256-B sub-row (a
+//    single chain per lane, 252-B gap tables), with prefix captures at record
+//    boundaries reduced by the same kind of inverse-shift tree (the file
+//    header of verify_rows.inc has the algebra).
+// Init/xorout enter once per record as a length-dependent constant.  No MFMA:
+// this is GF(2) arithmetic, not a contraction.
 //
 // Lookup tables live in LDS, replicated 32x so that lane (l & 31) always hits
 // bank (l & 31) for ds_read_b32: bank-conflict-free gathers whatever the data.
 // The LDS byte address of entry e for lane l is (e << 8) | ((l & 31) << 2)
-// | (region << 16), built by ONE v_perm_b32 per lookup.
+// | (region << 16), built by ONE v_perm_b32 per lookup.  The 128 KiB of
+// replicated tables (plus the tree tables) fill the CU's LDS, which is why the
+// rows are staged in a VGPR ring rather than in LDS.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -237,6 +250,21 @@ __device__ __forceinline__ uint32_t step_x(uint32_t x, uint32_t wn, LaneConst L,
     return xor3(xor3(ldsw<0>(tab, a0), ldsw<128>(tab, a1), ldsw<0>(tab, a2)), ldsw<128>(tab, a3), wn);
 }
 
+// The same step with ONE wait for its four lookups: an explicit lgkmcnt(0)
+// after the reads, before the first xor (the compiler otherwise waits twice,
+// lgkmcnt(1) then lgkmcnt(0)).  For a single dependent chain whose waves are
+// bound by instruction issue (k_verify_rows): one s_waitcnt fewer per step.
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // lgkmcnt(0) only
+__device__ __forceinline__ uint32_t step_x1(uint32_t x, uint32_t wn, LaneConst L, const uint32_t* tab) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, L.lc1, Sel<2>::v);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, L.lc1, Sel<3>::v);
+    const uint32_t t0 = ldsw<0>(tab, a0), t1 = ldsw<128>(tab, a1), t2 = ldsw<0>(tab, a2), t3 = ldsw<128>(tab, a3);
+    wait_lgkm0();
+    return xor3(xor3(t0, t1, t2), t3, wn);
+}
+
 // ---------------------------------------------------------------------------
 // Interleaved word streams with the gap folded into the tables (C2 k_full_blocks4,
 // C3 k_verify_rows).  A stream is the 32-bit words of a block at a fixed offset
@@ -316,6 +344,19 @@ __device__ __forceinline__ uint32_t tree_shift_xor(const uint32_t* shtab, uint32
 template <int L>
 __device__ __forceinline__ uint32_t tree_shift(const uint32_t* shtab, uint32_t v) {
     return tree_shift_xor<L>(shtab, v, 0u);
+}
+// tree_shift_xor with one wait for its four lookups (see step_x1).
+template <int L>
+__device__ __forceinline__ uint32_t tree_shift_xor1(const uint32_t* shtab, uint32_t v, uint32_t acc) {
+    const uint32_t* t = shtab + L * 1024;
+    const uint32_t t0 = t[v & 0xffu], t1 = t[256 + ((v >> 8) & 0xffu)], t2 = t[512 + ((v >> 16) & 0xffu)],
+                   t3 = t[768 + (v >> 24)];
+    wait_lgkm0();
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96), t3, acc, 0x96);
+}
+template <int L>
+__device__ __forceinline__ uint32_t tree_shift1(const uint32_t* shtab, uint32_t v) {
+    return tree_shift_xor1<L>(shtab, v, 0u);
 }
 
 template <int TM>

@@ -48,16 +48,28 @@ constexpr uint32_t kListStride = kListCap + 1;
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st, uint32_t* d_wsums = nullptr);
 // With d_wsums (count_wave_sums(nblocks) u32), the count pass also leaves the
-// records per 64 blocks; exclusive_scan_counts turns them and the counts into
-// the exclusive scan in one launch.
+// records per 64 blocks.
 uint64_t count_wave_sums(uint64_t nblocks);
-hipError_t exclusive_scan_counts(const DeviceInfo& di, const uint32_t* d_counts, uint32_t* d_first, uint64_t nblocks,
-                                 const uint32_t* d_wsums, hipStream_t st);
 // The verify kernel's list of qualifying blocks: kBlockListAux u32 (the list
-// length, the number of dense blocks, one row of kListPerBlock + 1 bucket
-// counts per workgroup of the ordering kernels), then nblocks u32.
+// length, the number of dense blocks, the number of blocks with more than
+// kListCap records, one row of kOrderRow counts per workgroup of the ordering
+// kernels: blocks with 1..kListPerBlock records, dense ones, ones past kListCap),
+// then nblocks u32.
 constexpr uint32_t kOrderMaxWG = 256;
-constexpr uint32_t kBlockListAux = 2 + kOrderMaxWG * (kListPerBlock + 1);
+constexpr uint32_t kOrderRow = kListPerBlock + 2;
+constexpr uint32_t kBlockListAux = 3 + kOrderMaxWG * kOrderRow;
+// The production count pass (revel_gpu_count_records / _count_scan_records):
+// counts, header lists and records per 64 blocks (d_wsums) as count_records,
+// plus the block order's bucket rows in aux (kBlockListAux + nblocks u32).
+// scan_order then turns them into the exclusive scan of the counts (d_first)
+// and the verify kernel's block list in aux: together with the count pass,
+// two launches for what count -> scan -> order histogram -> order scatter did in four.
+hipError_t count_hist(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                      uint64_t* d_hlist, uint32_t* d_wsums, uint32_t* d_aux, hipStream_t st);
+hipError_t scan_order(const DeviceInfo& di, uint64_t nbytes, const uint32_t* d_counts, const uint32_t* d_wsums,
+                      uint32_t* d_first, uint32_t* d_aux, hipStream_t st);
+// The block list of verify inside a header-list buffer (after the lists).
+uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks);
 // u64 words of a header-list buffer for nblocks: the lists, then the block list.
 uint64_t hlist_words(uint64_t nblocks);
 // d_tile_scratch: scan_scratch_words(n) u32 of device scratch.
@@ -82,10 +94,13 @@ hipError_t reasm_gather(const DeviceInfo& di, const void* d_image, uint64_t imag
 // hipErrorInvalidValue.  The experiment arms are in tools/experiments.
 hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_image, uint64_t nbytes,
                                uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                               const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st);
+                               const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st,
+                               bool list_ready = false);
+// list_ready: the count pass was count_hist + scan_order for this image, so
+// the block list in d_hlist's buffer is built (no ordering launches here).
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                          const uint32_t* d_counts, hipStream_t st);
+                          const uint32_t* d_counts, hipStream_t st, bool list_ready = false);
 
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
                              const uint32_t* d_counts, uint64_t nblocks, uint64_t* d_summary, hipStream_t st);
@@ -227,6 +242,7 @@ struct revel_gpu_context {
     const void* hlist_image = nullptr;
     uint64_t hlist_nbytes = 0;
     const uint32_t* hlist_counts = nullptr;
+    bool hlist_list_ready = false;  // the count pass also built verify's block list (count_scan_records)
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
     // per-64-block record sums of the last count pass (revel_gpu_count_records),

@@ -27,9 +27,52 @@ __device__ __forceinline__ Hdr header_in_window(uint3 w, uint32_t sh) {
 // kListCap headers (list_entry; the walk stops at the
 // first bad header, so only the last entry can be bad) followed by the in-block
 // offset of record kListCap when the block has more records.
-// With wsums (one wave per workgroup), wsums[w] = the records of blocks
-// [64 w, 64 w + 64): the first pass of the exclusive scan that follows
-// (revel_gpu_exclusive_scan_u32 on these counts skips its tile-sum launch).
+__device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ image, uint64_t nbytes, uint64_t b,
+                                                uint64_t* __restrict__ hlist) {
+    const uint64_t base = b * kBlockSize;
+    const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
+    const uint8_t* blk = image + base;
+    uint32_t n = 0;
+    if (bl >= 12u) {
+        // The next header's 12 B are loaded unconditionally, before this
+        // header's list store: loads and stores share vmcnt, so a store
+        // issued first would put its completion into every hop of the
+        // dependent walk.  Window address a = min(off & ~3, bl - 12): a window
+        // never reaches past the block (or the image end), and off - a <= 5
+        // keeps the 7 header bytes inside it.
+        const uint32_t cap = bl - 12u;
+        uint32_t off = 0, a = 0, resume = 0;
+        uint3 w = *reinterpret_cast<const uint3*>(blk);
+        for (;;) {
+            const Hdr h = header_in_window(w, off - a);
+            const bool ok = classify(h, off, bl) == REVEL_REC_OK;
+            const uint32_t next = off + kHeaderSize + h.len;  // <= bl when ok
+            const bool more = ok && bl - next >= kHeaderSize;
+            const uint32_t an = min(more ? next & ~3u : 0u, cap);
+            const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
+            // one unconditional store per hop (a store in a branch makes the
+            // compiler wait for it at the merge): entry n, or from record
+            // kListCap on the resume offset (rewritten with the same value)
+            resume = n == kListCap ? off : resume;
+            hlist[b * kListStride + min(n, kListCap)] = n < kListCap ? list_entry(h) : uint64_t(resume);
+            ++n;
+            if (!more) break;
+            off = next;
+            a = an;
+            w = wn;
+        }
+    } else if (bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
+        const Hdr h = read_header(blk, 0u, bl);
+        hlist[b * kListStride] = list_entry(h);
+        n = 1;
+    }
+    return n;
+}
+
+// One lane per block.  With wsums (one wave per workgroup), wsums[w] = the
+// records of blocks [64 w, 64 w + 64): the first pass of the exclusive scan
+// that follows.  (The replay and shard loaders' count pass; the C-ABI's is
+// k_count_hist, verify_rows.inc.)
 __global__ __launch_bounds__(64) void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                       uint32_t* __restrict__ counts, uint64_t* __restrict__ hlist,
                                                       uint32_t* __restrict__ wsums) {
@@ -38,43 +81,8 @@ __global__ __launch_bounds__(64) void k_count_records(const uint8_t* __restrict_
         const uint64_t b = b0 + threadIdx.x;
         uint32_t n = 0;
         if (b < nblocks) {
-        const uint64_t base = b * kBlockSize;
-        const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
-        const uint8_t* blk = image + base;
-        if (bl >= 12u) {
-            // The next header's 12 B are loaded unconditionally, before this
-            // header's list store: loads and stores share vmcnt, so a store
-            // issued first would put its completion into every hop of the
-            // dependent walk.  Window address a = min(off & ~3, bl - 12): a window
-            // never reaches past the block (or the image end), and off - a <= 5
-            // keeps the 7 header bytes inside it.
-            const uint32_t cap = bl - 12u;
-            uint32_t off = 0, a = 0, resume = 0;
-            uint3 w = *reinterpret_cast<const uint3*>(blk);
-            for (;;) {
-                const Hdr h = header_in_window(w, off - a);
-                const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-                const uint32_t next = off + kHeaderSize + h.len;  // <= bl when ok
-                const bool more = ok && bl - next >= kHeaderSize;
-                const uint32_t an = min(more ? next & ~3u : 0u, cap);
-                const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
-                // one unconditional store per hop (a store in a branch makes the
-                // compiler wait for it at the merge): entry n, or from record
-                // kListCap on the resume offset (rewritten with the same value)
-                resume = n == kListCap ? off : resume;
-                hlist[b * kListStride + min(n, kListCap)] = n < kListCap ? list_entry(h) : uint64_t(resume);
-                ++n;
-                if (!more) break;
-                off = next;
-                a = an;
-                w = wn;
-            }
-        } else if (bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
-            const Hdr h = read_header(blk, 0u, bl);
-            hlist[b * kListStride] = list_entry(h);
-            n = 1;
-        }
-        counts[b] = n;
+            n = count_block(image, nbytes, b, hlist);
+            counts[b] = n;
         }
         if (wsums) {
             uint32_t t = n;
@@ -1061,15 +1069,6 @@ hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nby
 
 uint64_t count_wave_sums(uint64_t nblocks) { return (nblocks + 63) / 64; }
 
-hipError_t exclusive_scan_counts(const DeviceInfo&, const uint32_t* d_counts, uint32_t* d_first, uint64_t nblocks,
-                                 const uint32_t* d_wsums, hipStream_t st) {
-    if (nblocks == 0) return hipSuccess;
-    const uint64_t tiles = (nblocks + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL((k_scan_apply<uint32_t, kScanTile / 64>), dim3((uint32_t)tiles), dim3(256), 0, st, d_counts,
-                       nblocks, d_wsums, d_first);
-    return hipGetLastError();
-}
-
 template <typename T>
 static hipError_t exclusive_scan_t(const T* d_in, T* d_out, uint64_t n, T* d_tile_scratch, hipStream_t st) {
     if (n == 0) return hipSuccess;
@@ -1171,7 +1170,8 @@ template <bool FRAME, bool ROWS = true, bool TQ = false, bool R64 = false, bool 
 static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                                       const uint32_t* d_first, revel_record_result* d_out, uint32_t lead,
                                       const uint64_t* hl, const uint32_t* d_counts, const uint64_t* xl, uint32_t xs,
-                                      hipStream_t st, uint32_t* d_blist = nullptr, const OverflowArgs* ov = nullptr) {
+                                      hipStream_t st, uint32_t* d_blist = nullptr, const OverflowArgs* ov = nullptr,
+                                      bool list_ready = false) {
     const uint64_t vbytes = nbytes + lead;
     const uint64_t b_lo = lead ? 1u : 0u;
     uint64_t b_hi = vbytes / kBlockSize;
@@ -1186,11 +1186,14 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
     if (b_hi > b_lo) {
         if constexpr (ROWS) {
             // qualifying blocks listed first, most records first (block_order)
-            hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, st, ov);
-            if (e != hipSuccess) return e;
+            if (!list_ready) {
+                hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, st);
+                if (e != hipSuccess) return e;
+            }
             hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + kBlockListAux,
-                               d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize);
+                               d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize,
+                               ov ? *ov : OverflowArgs{});
             dense_whole = d_blist + 1;
         } else {
             const uint64_t waves = kVerify2Threads / 64;
@@ -1223,7 +1226,7 @@ static uint32_t* block_list(const uint64_t* hl, uint64_t nblocks) {
 // tools/experiments (x_records.hip).
 hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_image, uint64_t nbytes,
                                uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
-                               const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st) {
+                               const uint64_t* d_hlist, const uint32_t* d_counts, hipStream_t st, bool list_ready) {
     if (path < 0 || path > 2) return hipErrorInvalidValue;
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     hipError_t e0 = ensure_len_tables(di, st);
@@ -1235,13 +1238,13 @@ hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_ima
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
     const bool split = path == 0 && hl && counts && aligned16(img);
     if (split) {
-        // k_order_hist lists the headers of blocks with more than kListCap
-        // records: its range is every block (lead 0, the partial tail included)
+        // k_verify_rows' prologue lists the headers of blocks with more than
+        // kListCap records: every block (lead 0, the partial tail included)
         const OverflowArgs ov{img, nbytes, d_first, hl, d_out};
         return launch_verify_split<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, counts,
                                           reinterpret_cast<const uint64_t*>(d_out),
                                           (uint32_t)(sizeof(revel_record_result) / 8), st, block_list(hl, nblocks),
-                                          &ov);
+                                          &ov, list_ready);
     }
     if (hl && counts) {
         // list the headers of blocks with more than kListCap records
@@ -1257,8 +1260,45 @@ hipError_t verify_records_path(const DeviceInfo& di, int path, const void* d_ima
 
 hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                           const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                          const uint32_t* d_counts, hipStream_t st) {
-    return verify_records_path(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st);
+                          const uint32_t* d_counts, hipStream_t st, bool list_ready) {
+    return verify_records_path(di, 0, d_image, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, st,
+                               list_ready);
+}
+
+uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks) { return block_list(d_hlist, nblocks); }
+
+// The grid of k_count_hist and k_scan_order (they must agree: the same
+// workgroup visits the same chunks in both) and the chunk visiting mask.
+static void count_grid(const DeviceInfo& di, uint64_t nblocks, uint32_t* grid, uint32_t* cmask) {
+    const uint64_t nchunks = (nblocks + 63) / 64;
+    uint64_t p = 1;
+    while (p < nchunks) p <<= 1;
+    *cmask = (uint32_t)(p - 1);
+    *grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(std::min<uint64_t>(kOrderMaxWG, (uint64_t)std::max(1, di.num_cu)),
+                              (p + kCountWaves - 1) / kCountWaves));
+}
+
+hipError_t count_hist(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                      uint64_t* d_hlist, uint32_t* d_wsums, uint32_t* d_aux, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    uint32_t grid, cmask;
+    count_grid(di, nblocks, &grid, &cmask);
+    hipLaunchKernelGGL(k_count_hist, dim3(grid), dim3(kCountThreads), 0, st, static_cast<const uint8_t*>(d_image),
+                       nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
+    return hipGetLastError();
+}
+
+hipError_t scan_order(const DeviceInfo& di, uint64_t nbytes, const uint32_t* d_counts, const uint32_t* d_wsums,
+                      uint32_t* d_first, uint32_t* d_aux, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    uint32_t grid, cmask;
+    count_grid(di, nblocks, &grid, &cmask);
+    hipLaunchKernelGGL(k_scan_order, dim3(grid), dim3(kCountThreads), 0, st, nbytes, d_counts, d_wsums, d_first, d_aux,
+                       cmask);
+    return hipGetLastError();
 }
 
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,

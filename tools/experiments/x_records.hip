@@ -151,6 +151,18 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
             if (variant == 26)
                 return launch_rows_shape<8, 1024, 2>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
             return launch_rows_shape<8, 1024, 3>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 31:  // DIAG: no captures, the row's table steps independent (latency probe)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 10>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 32:  // DIAG: the row's table steps independent, captures on (latency probe)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 8>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 33:  // DIAG: C2's block order (every block must qualify: probe images only)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 64>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 34:  // DIAG: C2's block order, no captures
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 66>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
         case 30:  // rows with eight captures per flush
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 0, 8>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
