@@ -432,6 +432,57 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks3(const uint8_t* __restr
     }
 }
 
+// The production C2 kernel (k_blocks.hip k_full_blocks4) with a scheduling
+// barrier after every row: each refill is issued in its own row, so ~15 rows
+// stay in flight through the block end (the production build's scheduler sinks
+// the last rows' refills to the block end, down to 4 in flight).
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_full_blocks4_sb(const uint8_t* __restrict__ blocks, uint64_t nblocks,
+                                                             uint32_t* __restrict__ masked_out,
+                                                             uint8_t* __restrict__ ok_out) {
+    __shared__ alignas(16) uint32_t tab[32768];
+    __shared__ uint32_t shtab[8 * 1024];
+    fill_gap_tables(tab, c_gap1020);
+    fill_inv_tree_tables(shtab, 8);
+    __syncthreads();
+    const LaneConst L = make_lane_const();
+    const uint32_t lane = lane_id();
+    const bool l0 = lane == 0;
+    const uint64_t waves_per_wg = THREADS / 64;
+    const uint64_t gwave = blockIdx.x * waves_per_wg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = gridDim.x * waves_per_wg;
+    if (gwave >= nblocks) return;
+    const uint8_t* lane_base = blocks + lane * 16u;
+    auto row = [&](uint64_t b, int g) {
+        b = b < nblocks ? b : nblocks - 1;
+        return ldg4(reinterpret_cast<const uint4*>(lane_base + b * kBlockSize + g * 1024));
+    };
+    uint4 ring[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) ring[g] = row(gwave, g);
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
+        uint32_t u0, u1, u2, u3;
+        uint4 hdr;
+#pragma unroll
+        for (int g = 0; g < 32; ++g) {
+            if (g == 0) {
+                uint4 c = ring[0];
+                zero_header_bytes(c, l0, false, &hdr);
+                u0 = c.x; u1 = c.y; u2 = c.z; u3 = c.w;
+                ring[0] = row(b, 16);
+            }
+            const uint4 wn = g < 31 ? ring[(g + 1) & 15] : make_uint4(0, 0, 0, 0);
+            u0 = step_x(u0, wn.x, L, tab);
+            u1 = step_x(u1, wn.y, L, tab);
+            u2 = step_x(u2, wn.z, L, tab);
+            u3 = step_x(u3, wn.w, L, tab);
+            if (g < 31) ring[(g + 1) & 15] = g + 17 < 32 ? row(b, g + 17) : row(b + nwaves, g + 17 - 32);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        finish_full_block<false>(u0, u1, u2, u3, hdr, b, shtab, lane, masked_out, ok_out, nullptr);
+    }
+}
+
 template <int THREADS, bool NT, bool FRAME, bool XS = false>
 hipError_t launch_full3(const DeviceInfo& di, const uint8_t* blocks, uint64_t n, uint32_t* masked, uint8_t* ok,
                         uint8_t* frame_dst, hipStream_t st) {
@@ -491,6 +542,13 @@ extern "C" int revel_x_crc_full_blocks_variant(revel_gpu_context* ctx, int varia
         case 21: e = launch_full3<1024, false, false>(di, b, n, d_masked, d_ok, nullptr, st); break;
         // v3 with the x-state chain (3-input xors)
         case 22: e = launch_full3<1024, true, false, true>(di, b, n, d_masked, d_ok, nullptr, st); break;
+        // production C2 with a scheduling barrier per row (constant ring depth)
+        case 23: {
+            const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (n + 15) / 16));
+            hipLaunchKernelGGL(k_full_blocks4_sb<1024>, dim3((uint32_t)grid), dim3(1024), 0, st, b, n, d_masked, d_ok);
+            e = hipGetLastError();
+            break;
+        }
         // v1: lane-owned 512-B chunks
         case 1: e = launch_full<TM_S2R, 512, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st); break;
         case 2: e = launch_full<TM_S4R, 256, LM_STAGED, false>(di, 1, b, n, d_masked, d_ok, nullptr, st); break;

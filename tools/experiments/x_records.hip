@@ -163,6 +163,78 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
         case 34:  // DIAG: C2's block order, no captures
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 66>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 35:  // DIAG: loads + XOR fold only (no steps, captures or multiplies), 8-row ring
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 131>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 36:  // DIAG: loads + XOR fold only, 16-row ring
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 1024, 131>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 37:  // DIAG: no row transposes
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 256>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 38:  // DIAG: no captures, 16-row ring (control: 26)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 1024, 2>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 39:  // DIAG: loads + XOR fold only, C2's block order (probe images only)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 195>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 40:  // DIAG: loads + XOR fold only, global loads, 8-row ring
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 643>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 41:  // DIAG: loads + XOR fold only, global loads, 16-row ring
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 1024, 643>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 42:  // DIAG: loads + XOR fold only, global loads, C2's block order
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 707>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 43:  // DIAG: the row loop alone (no per-block work), sorted order
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 7299>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 44:  // DIAG: the row loop alone, C2's order
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 7363>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 45:  // DIAG: the row loop alone, C2's order, 16-row ring
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<16, 1024, 7363>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 46:  // DIAG: loads-only, no finalizer (setup + prefetch kept)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 1155>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 47:  // DIAG: loads-only, no setup / prefetch (finalizer kept)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 6275>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 48:  // DIAG: loads-only, prefetch kept (no setup, no finalizer)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 3203>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 49:  // part 0 peeled out of the part loop
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 8192>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 50:  // DIAG: loads-only, part 0 peeled
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 8323>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 51:  // DIAG: loads-only, no result stores
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 16515>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 52:  // DIAG: loads-only, no finalizer-constant gathers
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 32899>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 53:  // DIAG: loads-only, neither
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 49283>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 54:  // DIAG: full compute, no result stores
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 16384>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 55:  // result stores deferred into the next block's part 0
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 65536>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 56:  // DIAG: nontemporal result stores
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 131072>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 57:  // DIAG: 8 B per record stored
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 262144>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 58:  // DIAG: result stores into per-wave private slots
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 524288>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
         case 30:  // rows with eight captures per flush
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 0, 8>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
