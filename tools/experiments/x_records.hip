@@ -40,7 +40,8 @@ uint32_t grid_for(const DeviceInfo& di, uint64_t n, uint64_t waves) {
 template <int RING, int THREADS, int DIAG = 0, int NB = 4>
 hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t nbytes, uint64_t base_offset,
                              const uint32_t* d_first, revel_record_result* d_out, const uint64_t* hl,
-                             const uint32_t* d_counts, const uint64_t* xl, uint32_t xs, hipStream_t st) {
+                             const uint32_t* d_counts, const uint64_t* xl, uint32_t xs, hipStream_t st,
+                             revel_record_result* rows_out = nullptr) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     const uint64_t b_hi = nbytes / kBlockSize;
     uint32_t* d_blist = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(hl) + nblocks * kListStride);
@@ -48,8 +49,8 @@ hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t 
         hipError_t e = launch_block_order(di, d_counts, 0u, (uint32_t)b_hi, d_blist, st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_verify_rows<false, RING, THREADS, DIAG, NB>), dim3((uint32_t)std::max(1, di.num_cu)),
-                           dim3(THREADS), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl,
-                           d_blist + kBlockListAux, d_blist);
+                           dim3(THREADS), 0, st, img, base_offset, d_first, rows_out ? rows_out : d_out, 0u, hl,
+                           d_counts, xl, d_blist + kBlockListAux, d_blist);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -235,6 +236,30 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
         case 58:  // DIAG: result stores into per-wave private slots
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 524288>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 59:  // DIAG: results into a private line-aligned 64-slot region per block, all 64 lanes (whole lines)
+        case 60: {  // DIAG: the same region, lanes < n only (partial last line)
+            if (!lists) return hipErrorInvalidValue;
+            static revel_record_result* pad = nullptr;  // scratch of 64 results per block (timing only)
+            static uint64_t pad_blocks = 0;
+            if (pad_blocks < nblocks) {
+                if (pad) (void)hipFree(pad);
+                pad = nullptr;
+                hipError_t e = hipMalloc(&pad, nblocks * 64 * sizeof(revel_record_result));
+                if (e != hipSuccess) return e;
+                pad_blocks = nblocks;
+            }
+            if (variant == 59)
+                return launch_rows_shape<8, 1024, 1048576>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl,
+                                                           xs, st, pad);
+            return launch_rows_shape<8, 1024, 2097152>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs,
+                                                       st, pad);
+        }
+        case 61:  // DIAG: 4 B per record into the block's spare header-list slots (timing only)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 4194304>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 62:  // DIAG: 4 B per record, a contiguous u32 array in record order (timing only)
+            if (!lists) return hipErrorInvalidValue;
+            return launch_rows_shape<8, 1024, 8388608>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
         case 30:  // rows with eight captures per flush
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 0, 8>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
