@@ -1195,6 +1195,12 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
                                d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize,
                                ov ? *ov : OverflowArgs{});
             dense_whole = d_blist + 1;
+            if constexpr (!FRAME) {
+                hipError_t e = launch_expand_rows(di, base_offset, lead, d_first, d_out, hl, d_counts, (uint32_t)b_lo,
+                                                  (uint32_t)b_hi, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize,
+                                                  st);
+                if (e != hipSuccess) return e;
+            }
         } else {
             const uint64_t waves = kVerify2Threads / 64;
             const uint32_t grid = (uint32_t)std::max<uint64_t>(

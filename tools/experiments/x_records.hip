@@ -7,6 +7,8 @@
 // ring.  Results: profiles/r1*_c3_*.txt, r2_c3_v7_vs_v3.txt; DESIGN.md section
 // 4.2.  Symbols are hidden except revel_x_verify_records_variant; the device
 // tables are this module's own copies (filled by its own k_init_len_tables).
+#include <vector>
+
 #include "k_records.hip"
 
 namespace {
@@ -53,6 +55,11 @@ hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t 
                            d_counts, xl, d_blist + kBlockListAux, d_blist);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
+        if constexpr (DIAG == 0) {  // the production kernel leaves its results to the expander
+            e = launch_expand_rows(di, base_offset, 0u, d_first, d_out, hl, d_counts, 0u, (uint32_t)b_hi, 0xFFFFFFFFu,
+                                   kBlockSize, st);
+            if (e != hipSuccess) return e;
+        }
     }
     return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl, xs, st);
 }
@@ -260,6 +267,40 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
         case 62:  // DIAG: 4 B per record, a contiguous u32 array in record order (timing only)
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 8388608>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);
+        case 63: {  // DIAG: 4 B per record into a list-order staging array (offsets made on the host; timing only)
+            if (!lists || !b_hi) return hipErrorInvalidValue;
+            uint32_t* d_blist = block_list_of(const_cast<uint64_t*>(hl), nblocks);
+            hipError_t e = launch_block_order(di, d_counts, 0u, (uint32_t)b_hi, d_blist, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            uint32_t len = 0;
+            e = hipMemcpy(&len, d_blist, 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return e;
+            std::vector<uint32_t> list(len), cnt(nblocks), off(len + 1);
+            if (len) e = hipMemcpy(list.data(), d_blist + kBlockListAux, 4ull * len, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(cnt.data(), d_counts, 4ull * nblocks, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return e;
+            off[0] = 0;
+            for (uint32_t k = 0; k < len; ++k) off[k + 1] = off[k] + cnt[list[k]];
+            static uint32_t* d_off = nullptr;
+            static uint64_t off_cap = 0;
+            if (off_cap < len + 1) {
+                if (d_off) (void)hipFree(d_off);
+                d_off = nullptr;
+                e = hipMalloc(&d_off, 4ull * (len + 1));
+                if (e != hipSuccess) return e;
+                off_cap = len + 1;
+            }
+            e = hipMemcpy(d_off, off.data(), 4ull * (len + 1), hipMemcpyHostToDevice);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_verify_rows<false, 8, 1024, 16777216, 4>), dim3((uint32_t)std::max(1, di.num_cu)),
+                               dim3(1024), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts,
+                               reinterpret_cast<const uint64_t*>(d_off), d_blist + kBlockListAux, d_blist);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl, xs,
+                                                   st);
+        }
         case 30:  // rows with eight captures per flush
             if (!lists) return hipErrorInvalidValue;
             return launch_rows_shape<8, 1024, 0, 8>(di, img, nbytes, base_offset, d_first, d_out, hl, d_counts, xl, xs, st);

@@ -6,7 +6,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$1; mkdir -p "$O"
 S=$R/tools/box_step.sh
-$S 300 "$O/zipf.log" python3 "$R/tools/bench_c3.py" --variants ${VARS:-24,54,56,59,60} --rounds 3 --iters 3 || exit 99
+$S 300 "$O/zipf.log" python3 "$R/tools/bench_c3.py" --variants ${VARS:-24,54,56,59,60} --rounds ${ROUNDS:-3} --iters 3 || exit 99
 grep -h verify_variant "$O/zipf.log" | python3 -c '
 import json,sys
 for l in sys.stdin:
