@@ -272,6 +272,33 @@ def test_verify_and_append_64_record_blocks(gpu_ctx, trailer):
     assert gpu_ctx.d2h(out, n).tobytes() == img
 
 
+def test_expander_counts_1_to_64_with_flips(gpu_ctx):
+    """k_expand_rows (round 3): the rows kernel leaves a mismatch mask per block
+    and the expander writes the results, one lane per record across 16-block
+    chunks in 64-record passes.  Blocks whose record counts cycle through
+    1..64 (so chunks and passes split blocks everywhere, records 32..63 use the
+    mask's high word) with ~1 record in 8 corrupted at a random byte, plus a
+    torn last header: every field equals the oracle walk on every verify path."""
+    rng = np.random.default_rng(6464)
+    recs = []
+    for nrec in list(range(1, 65)) + list(range(64, 0, -7)):
+        body = 32768 - 7 * nrec - int(rng.integers(0, 7))  # a trailer of 0..6 bytes
+        cuts = np.sort(rng.choice(np.arange(1, body), nrec - 1, replace=False)) if nrec > 1 else np.array([], int)
+        sizes = np.diff(np.concatenate([[0], cuts, [body]]))
+        recs += [rng.integers(0, 256, int(sz), dtype=np.uint8).tobytes() for sz in sizes]
+    img = bytearray(oc.write_image(recs))
+    ref0 = oc.walk(bytes(img))
+    for i in np.flatnonzero(rng.random(len(ref0)) < 0.125):
+        o, n = int(ref0["file_offset"][i]), int(ref0["length"][i])
+        img[o + 7 + int(rng.integers(0, max(1, n)))] ^= 1 << int(rng.integers(0, 8))
+    img = bytes(img) + bytes([0x11, 0x22, 0x33])  # a torn header at the end
+    ref = oc.walk(img)
+    assert int((ref["status"] == 1).sum()) > 100
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)
+
+
 def test_verify_small_records_dense(gpu_ctx):
     """Thousands of tiny records per block (many batches of the LDS record
     list, record starts/ends in every lane) in random bit positions."""
