@@ -398,7 +398,7 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
     }
 
 
-def c3_records(ctx, D, gib: float, iters: int = 5):
+def c3_records(ctx, D, gib: float, iters: int = 9):
     """Config C3 on every rank: Zipf(1.1) record sizes 64*k, k in [1, 512]
     (seed 0x5EED0003 ^ rank), framed ON DEVICE by revel_gpu_append_records
     (bit-exact with log::Writer, tests/test_gpu.py) from device-generated
