@@ -81,11 +81,31 @@ class GuardedImage:
         self.ptr = self.va
 
     def free(self):
+        """Deferred to the end of the module (release_all): an image released
+        here lets the next test's allocation reuse its physical pages, and one
+        run read the previous test's data through them (lines written by a
+        kernel into memory of this API were not written back before the
+        release, it seems) -- so no physical page is reused within the module."""
+        _LIVE.append(self)
+
+    def release(self):
         if self.va:
             self.hip.hipMemUnmap(self.va, self.nbytes)
             self.hip.hipMemRelease(self.handle)
             self.hip.hipMemAddressFree(self.va, self.reserved)
             self.va = self.ptr = None
+
+
+_LIVE = []
+
+
+@pytest.fixture(scope="module", autouse=True)
+def release_all():
+    yield
+    import ctypes as _c
+    _c.CDLL("libamdhip64.so").hipDeviceSynchronize()
+    while _LIVE:
+        _LIVE.pop().release()
 
 
 def _guarded_nbytes(min_blocks: int) -> int:
@@ -109,6 +129,29 @@ def dense_tail_records(nbytes: int):
     recs += [rng.integers(0, 256, 120, dtype=np.uint8).tobytes() for _ in range(257)]
     recs.append(rng.integers(0, 256, 122, dtype=np.uint8).tobytes())
     return recs
+
+
+def test_full_blocks_end_at_unmapped_granule(gpu_ctx):
+    """The C2 kernel's ring re-reads the last block past the end of the list:
+    its loads stay inside the image."""
+    nbytes = _guarded_nbytes(2)
+    n = nbytes // BLOCK_SIZE
+    # the blocks come from the host, as in the dense test: one r3 run copied
+    # the 64-KiB guarded range back after a device-side synth and got the
+    # bytes it held before the synth (a D2H copy of virtual-memory-API memory
+    # that did not see lines still dirty in L2, it seems); what this test is
+    # about is the C2 kernel's loads, so no device write precedes a D2H here
+    host = oc.synth_full_blocks(n, seed=0x5EED0002)
+    g = GuardedImage(0, nbytes)
+    try:
+        gpu_ctx.h2d(g, host.reshape(-1))
+        m, ok = gpu_ctx.alloc(4 * n), gpu_ctx.alloc(n)
+        gpu_ctx.crc_full_blocks(g, n, m, ok)
+        gpu_ctx.sync()
+        assert np.array_equal(gpu_ctx.d2h(m, 4 * n, np.uint32), oc.full_block_crcs(host))
+        assert gpu_ctx.d2h(ok, n).all()
+    finally:
+        g.free()
 
 
 def test_dense_last_block_ends_at_unmapped_granule(gpu_ctx):
@@ -153,28 +196,5 @@ def test_append_framing_dense_last_block_into_guarded_image(gpu_ctx):
                                          g.ptr, nbytes, ctypes.byref(n), None))
         assert n.value == nbytes
         assert bytes(gpu_ctx.d2h(g, nbytes)) == want
-    finally:
-        g.free()
-
-
-def test_full_blocks_end_at_unmapped_granule(gpu_ctx):
-    """The C2 kernel's ring re-reads the last block past the end of the list:
-    its loads stay inside the image."""
-    nbytes = _guarded_nbytes(2)
-    n = nbytes // BLOCK_SIZE
-    # the blocks come from the host, as in the dense test: one r3 run copied
-    # the 64-KiB guarded range back after a device-side synth and got the
-    # bytes it held before the synth (a D2H copy of virtual-memory-API memory
-    # that did not see lines still dirty in L2, it seems); what this test is
-    # about is the C2 kernel's loads, so no device write precedes a D2H here
-    host = oc.synth_full_blocks(n, seed=0x5EED0002)
-    g = GuardedImage(0, nbytes)
-    try:
-        gpu_ctx.h2d(g, host.reshape(-1))
-        m, ok = gpu_ctx.alloc(4 * n), gpu_ctx.alloc(n)
-        gpu_ctx.crc_full_blocks(g, n, m, ok)
-        gpu_ctx.sync()
-        assert np.array_equal(gpu_ctx.d2h(m, 4 * n, np.uint32), oc.full_block_crcs(host))
-        assert gpu_ctx.d2h(ok, n).all()
     finally:
         g.free()
