@@ -42,6 +42,8 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
         // keeps the 7 header bytes inside it.
         const uint32_t cap = bl - 12u;
         uint32_t off = 0, a = 0, resume = 0;
+        uint64_t pend = 0;
+        uint64_t* const hl = hlist + b * kListStride;
         uint3 w = *reinterpret_cast<const uint3*>(blk);
         for (;;) {
             const Hdr h = header_in_window(w, off - a);
@@ -50,17 +52,31 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
             const bool more = ok && bl - next >= kHeaderSize;
             const uint32_t an = min(more ? next & ~3u : 0u, cap);
             const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
-            // one unconditional store per hop (a store in a branch makes the
-            // compiler wait for it at the merge): entry n, or from record
-            // kListCap on the resume offset (rewritten with the same value)
-            resume = n == kListCap ? off : resume;
-            hlist[b * kListStride + min(n, kListCap)] = n < kListCap ? list_entry(h) : uint64_t(resume);
+            // The lanes still walking all stand at the same hop n (they start
+            // together and take one hop per iteration), so n's parity is
+            // wave-uniform: entries are stored in pairs (one 16-B store every
+            // other hop -- the walk is bound by the address unit, TA busy
+            // ~80 %), from record kListCap on the resume offset alone.
+            const uint32_t nu = __builtin_amdgcn_readfirstlane(n);
+            const uint64_t e = list_entry(h);
+            if (nu < kListCap) {
+                if (nu & 1u) {
+                    const uint64_t pair[2] = {pend, e};
+                    __builtin_memcpy(hl + (n - 1u), pair, 16);
+                } else {
+                    pend = e;
+                }
+            } else {
+                resume = n == kListCap ? off : resume;
+                hl[kListCap] = uint64_t(resume);
+            }
             ++n;
             if (!more) break;
             off = next;
             a = an;
             w = wn;
         }
+        if ((n & 1u) && n <= kListCap) hl[n - 1u] = pend;  // the last entry of an odd count
     } else if (bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
         const Hdr h = read_header(blk, 0u, bl);
         hlist[b * kListStride] = list_entry(h);
