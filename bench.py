@@ -59,6 +59,8 @@ def parse(argv=None):
                     help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
+    ap.add_argument("--c3-small-gib", type=float, default=1.0,
+                    help="per-rank device-framed image of 64..256 B records for the c3_small field (0 = skip)")
     ap.add_argument("--share-gpus", action="store_true",
                     help="rehearsal: allow more ranks than GPUs (rank r drives GPU r mod count)")
     ap.add_argument("--dry-run", action="store_true",
@@ -296,28 +298,24 @@ def c1_reference_path(oracle_c):
             "note": "reference's own reader cannot complete C1 (SURVEY App. A #1-3); LevelDB-correct walk timed"}
 
 
-def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
-    """Config C5, PCIe-inclusive (not `value`): ONE WAL file on the host holds
-    every rank's blocks (rank r's `gib` GiB at offset r * gib); each rank loads
-    its block-aligned shard of it onto its GPU (revel_gpu_wal_shard_load: mmap
-    of the file -> 8 fill threads -> 3 x 64 MiB pinned ring -> H2D on a copy
-    stream, records counted as each window lands -> verify of the resident
-    shard), the ranks exchange their boundary blobs and rank 0 stitches them
-    (revel_wal_stitch_new).  Rate = file bytes / max-over-ranks load time;
-    file writing is outside the clock.  The file was just written, so it is
-    read from the page cache.  `value` times the pipeline (first window read ->
-    boundary blob); `all_in_GiB_s` adds the shard's HBM + pinned-ring setup."""
+def e2e_file_path(D) -> tuple:
+    """(directory, path) of the one WAL file every rank of this job shares."""
     import tempfile
-    from revel_amd import shard
-    k = min(nblocks, int(gib * (1 << 30)) // BLOCK_SIZE)
-    per = k * BLOCK_SIZE
-    total = per * D.world
     d = os.environ.get("REVEL_BENCH_DIR") or tempfile.gettempdir()
     tag = os.environ.get("TORCHELASTIC_RUN_ID") or str(os.getppid() if D.world > 1 else os.getpid())
-    path = os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{tag}.log")
-    # every rank must see the same file on this host: a failure anywhere (no
-    # space, a write error) makes every rank skip this leg together -- the
-    # headline value is already measured and must still be printed
+    return d, os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{tag}.log")
+
+
+def e2e_write_file(D, per: int, part):
+    """Write the shared WAL file for the end_to_end leg: rank 0 checks the
+    free space for all ranks' parts (world x per bytes + 1 GiB) and creates
+    the file, then every rank writes its part (part() -> bytes of length per)
+    at rank x per.  A failure anywhere makes EVERY rank skip the leg together
+    (the headline value is already measured and must still be printed).
+    Returns (path, None), or (None, reason) after removing the file.
+    REVEL_BENCH_E2E_FAIL_RANK=r makes rank r's write fail (CPU tests)."""
+    d, path = e2e_file_path(D)
+    total = per * D.world
     why = ""
     if D.rank == 0:
         try:
@@ -330,10 +328,12 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
         except OSError as ex:
             why = f"create {path}: {ex}"
     if D.max(float(bool(why))) > 0:
-        return {"value": None, "skipped": why or "another rank could not write its part"}
+        return None, why or "another rank could not write its part"
     ok = True
-    host = ctx.d2h(dblocks, per)  # this rank's part of the WAL = its first k device blocks
     try:
+        if os.environ.get("REVEL_BENCH_E2E_FAIL_RANK") == str(D.rank):
+            raise OSError(28, "injected write failure (REVEL_BENCH_E2E_FAIL_RANK)")
+        host = part()
         fd = os.open(path, os.O_WRONLY)
         try:
             view = memoryview(host)
@@ -342,9 +342,9 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
                 done += os.pwrite(fd, view[done:], D.rank * per + done)
         finally:
             os.close(fd)
+        del host, view
     except OSError as ex:
         ok, why = False, f"rank {D.rank} write: {ex}"
-    del host
     if D.max(float(not ok)) > 0:
         D.barrier()
         if D.rank == 0:
@@ -352,7 +352,29 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
                 os.unlink(path)
             except OSError:
                 pass
-        return {"value": None, "skipped": why or "another rank could not write its part"}
+        return None, why or "another rank could not write its part"
+    return path, None
+
+
+def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
+    """Config C5, PCIe-inclusive (not `value`): ONE WAL file on the host holds
+    every rank's blocks (rank r's `gib` GiB at offset r * gib); each rank loads
+    its block-aligned shard of it onto its GPU (revel_gpu_wal_shard_load: mmap
+    of the file -> 8 fill threads -> 3 x 64 MiB pinned ring -> H2D on a copy
+    stream, records counted as each window lands -> verify of the resident
+    shard), the ranks exchange their boundary blobs and rank 0 stitches them
+    (revel_wal_stitch_new).  Rate = file bytes / max-over-ranks load time;
+    file writing is outside the clock.  The file was just written, so it is
+    read from the page cache.  `value` times the pipeline (first window read ->
+    boundary blob); `all_in_GiB_s` adds the shard's HBM + pinned-ring setup."""
+    from revel_amd import shard
+    k = min(nblocks, int(gib * (1 << 30)) // BLOCK_SIZE)
+    per = k * BLOCK_SIZE
+    total = per * D.world
+    # this rank's part of the WAL = its first k device blocks
+    path, why = e2e_write_file(D, per, lambda: ctx.d2h(dblocks, per))
+    if path is None:
+        return {"value": None, "skipped": why}
     D.barrier()
     s, e = shard.block_ranges(total, D.world)[D.rank]
     t0 = time.perf_counter()
@@ -392,42 +414,59 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
         "physical_records": summ.get("physical"),
         "bad_records": summ.get("bad"),
         "stitched": summ.get("stitched"),
-        "source": f"one WAL file in {d} (page cache: written just before), shared by all ranks",
+        "source": f"one WAL file in {os.path.dirname(path)} (page cache: written just before), shared by all ranks",
         "path": "file mmap -> 8 fill threads -> 3 x 64 MiB pinned ring -> H2D (copy stream) + per-window record count "
                 "-> verify of the HBM-resident shard -> boundary blob -> rank-0 stitch",
     }
 
 
-def c3_records(ctx, D, gib: float, iters: int = 9):
-    """Config C3 on every rank: Zipf(1.1) record sizes 64*k, k in [1, 512]
-    (seed 0x5EED0003 ^ rank), framed ON DEVICE by revel_gpu_append_records
-    (bit-exact with log::Writer, tests/test_gpu.py) from device-generated
-    payload bytes, then the production verify path (count -> scan -> verify)
-    timed with HIP events; all ranks start together, rate = total bytes /
-    max-over-ranks median time."""
-    import numpy as np
+def c3_sizes(shape: str, seed: int, target: int) -> np.ndarray:
+    """Record sizes for the device-framed verify legs, until the framed image
+    reaches `target` bytes.  zipf (C3): 64*k B, k in [1, 512] ~ Zipf(1.1);
+    small: 64..256 B uniform -- the db_bench-shaped logs DB::put produces
+    through DB::write -> Writer::add_record (db.rs:95-120, log_writer.rs:58-97),
+    ~200 records per block, so nearly every block takes the dense path."""
+    rng = np.random.default_rng(seed)
+    if shape == "zipf":
+        k = np.arange(1, 513)
+        p = k ** -1.1
+        p /= p.sum()
+        sizes = (64 * rng.choice(k, size=target // 3000 + 4096, p=p)).astype(np.uint64)
+    elif shape == "small":
+        sizes = rng.integers(64, 257, size=target // 160 + 4096).astype(np.uint64)
+    else:
+        raise ValueError(shape)
+    return sizes[:int(np.searchsorted(np.cumsum(sizes + 7), target))]
+
+
+def c3_image(ctx, shape: str, seed: int, gib: float):
+    """A device-framed WAL image: payload bytes synthesised on the device,
+    framed by revel_gpu_append_records (bit-exact with log::Writer,
+    tests/test_gpu.py).  Returns (image buffer, image bytes, record count)."""
+    sizes = c3_sizes(shape, seed, int(gib * (1 << 30)))
+    nb_pay = (int(sizes.sum()) + BLOCK_SIZE - 1) // BLOCK_SIZE
+    pay = ctx.alloc(max(1, nb_pay) * BLOCK_SIZE)
+    ctx.synth_full_blocks(pay, nb_pay, seed=seed)
+    img, n, _ = ctx.append_records(pay, sizes)
+    pay.free()
+    return img, n, len(sizes)
+
+
+def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: None):
+    """The production verify of a resident image through the C-ABI
+    (revel_gpu_count_scan_records -> revel_gpu_verify_records), timed with
+    HIP events around both calls, `iters` times.  Returns (per-iteration ms,
+    physical records, records whose status is not OK)."""
     from revel_amd._lib import check, lib
     from revel_amd.gpu import RECORD_DTYPE
     L = lib()
-    rng = np.random.default_rng(0x5EED0003 ^ D.rank)
-    k = np.arange(1, 513)
-    p = k ** -1.1
-    p /= p.sum()
-    target = int(gib * (1 << 30))
-    sizes = (64 * rng.choice(k, size=target // 3000 + 4096, p=p)).astype(np.uint64)
-    sizes = sizes[:int(np.searchsorted(np.cumsum(sizes + 7), target))]
-    nb_pay = (int(sizes.sum()) + BLOCK_SIZE - 1) // BLOCK_SIZE
-    pay = ctx.alloc(nb_pay * BLOCK_SIZE)
-    ctx.synth_full_blocks(pay, nb_pay, seed=0x5EED0003 ^ D.rank)
-    img, n, _ = ctx.append_records(pay, sizes)
-    pay.free()
     nblocks = (n + BLOCK_SIZE - 1) // BLOCK_SIZE
     counts, first = ctx.alloc(4 * nblocks), ctx.alloc(4 * nblocks)
-    cap = len(sizes) + 2 * nblocks + 64           # records + FIRST/MIDDLE/LAST splits
+    cap = nrec + 2 * nblocks + 64           # records + FIRST/MIDDLE/LAST splits
     out = ctx.alloc(cap * RECORD_DTYPE.itemsize)
     e0, e1 = ctx.event(), ctx.event()
     times = []
-    D.barrier()
+    barrier()
     for _ in range(iters):
         e0.record()
         check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
@@ -435,14 +474,28 @@ def c3_records(ctx, D, gib: float, iters: int = 9):
         e1.record()
         ctx.sync()
         times.append(e0.elapsed_ms(e1))
-    D.barrier()
+    barrier()
     nphys = int(ctx.d2h(first, 4 * nblocks, np.uint32)[-1]) + int(ctx.d2h(counts, 4 * nblocks, np.uint32)[-1])
     res = ctx.d2h(out, nphys * RECORD_DTYPE.itemsize).view(RECORD_DTYPE)
-    bad = D.sum(float((res["status"] != 0).sum()))
+    bad = int((res["status"] != 0).sum())
+    for b in (counts, first, out):
+        b.free()
+    return times, nphys, bad
+
+
+def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
+    """Config C3 on every rank (shape zipf: Zipf(1.1) record sizes 64*k, k in
+    [1, 512], seed 0x5EED0003 ^ rank; shape small: 64..256 B, the c3_small
+    field), framed ON DEVICE, then the production verify path (count -> scan
+    -> verify) timed with HIP events; all ranks start together, rate = total
+    bytes / max-over-ranks median time."""
+    seed = (0x5EED0003 if shape == "zipf" else 0x5EED0005) ^ D.rank
+    img, n, nrec = c3_image(ctx, shape, seed, gib)
+    times, nphys, bad = c3_verify_timed(ctx, img, n, nrec, iters, D.barrier)
+    img.free()
+    bad = D.sum(float(bad))
     ms = float(np.median(times))
     ms_max = D.max(ms)
-    for b in (img, counts, first, out):
-        b.free()
     return {
         "unit": "GiB/s",
         "value": round(n * D.world / 2**30 / (ms_max / 1e3), 1),
@@ -452,8 +505,9 @@ def c3_records(ctx, D, gib: float, iters: int = 9):
         "bad_records": int(bad),
         "alg_GB_s_rank0": round((n + 24 * nphys) / (ms / 1e3) / 1e9, 1),
         "path": "count (per-block header walk + header list) -> scan -> verify (production: k_verify_rows over blocks "
-                "with <= 64 records, k_verify_records_dense over denser ones, single-wave partial blocks)",
-        "data": "Zipf(1.1) 64 B..32 KiB records framed on device by revel_gpu_append_records",
+                "with <= 64 records, k_verify_records_dense over denser ones)",
+        "data": ("Zipf(1.1) 64 B..32 KiB records" if shape == "zipf" else "uniform 64..256 B records (db_bench-shaped)")
+                + " framed on device by revel_gpu_append_records",
     }
 
 
@@ -524,6 +578,9 @@ def main(argv=None):
     c3 = None
     if args.c3_gib > 0:
         c3 = c3_records(ctx, D, args.c3_gib)
+    c3_small = None
+    if args.c3_small_gib > 0:
+        c3_small = c3_records(ctx, D, args.c3_small_gib, shape="small")
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu:
@@ -532,7 +589,9 @@ def main(argv=None):
     if D.rank == 0:
         out = result_line(args, D, ranks, value=round(value, 1), ms=round(wall / args.steps * 1e3, 4))
         out["config"].update({"kernel_variant": "production" if args.variant is None else args.variant,
-                              "all_verify_flags_ok": all_ok})
+                              "all_verify_flags_ok": all_ok,
+                              "library_sha256": library_sha256(),   # which binary ran (build provenance)
+                              "build_info": gpu.build_info()})
         out["roofline"] = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -547,6 +606,7 @@ def main(argv=None):
         out["cpu_baseline"] = cpu
         out["end_to_end"] = e2e
         out["c3"] = c3
+        out["c3_small"] = c3_small
         print(json.dumps(out), flush=True)
     D.close()
     return 0
@@ -583,13 +643,28 @@ def result_line(args, D, ranks, value, ms):
 
 def dry_run(args, D):
     """The launcher and the distributed plumbing without a GPU: every rank
-    reports itself, rank 0 prints the line with null values."""
+    reports itself, rank 0 prints the line with null values.  With --e2e-gib
+    the end_to_end leg's shared-file logic runs for real (free-space check of
+    world x per-rank bytes, every rank's part written, the all-ranks skip on
+    any failure) with zero bytes in place of the device blocks."""
     D.barrier()
+    e2e = None
+    if args.e2e_gib > 0:
+        k = min(args.blocks, int(args.e2e_gib * (1 << 30)) // BLOCK_SIZE)
+        per = k * BLOCK_SIZE
+        path, why = e2e_write_file(D, per, lambda: np.zeros(per, np.uint8))
+        size = os.path.getsize(path) if path else None
+        D.barrier()
+        if path and D.rank == 0:
+            os.unlink(path)
+        e2e = {"file_bytes": per * D.world, "per_rank_bytes": per, "skipped": why,
+               "per_rank": D.gather({"rank": D.rank, "skipped": path is None, "file_size_seen": size})}
     ranks = D.gather({"rank": D.rank, "local_rank": D.local, "host": socket.gethostname(), "device": D.local,
                       "pci_bus_id": f"dry-run-{D.local}", "kernel_ms": None})
     if D.rank == 0:
         out = result_line(args, D, ranks, value=None, ms=None)
         out["dry_run"] = True
+        out["end_to_end"] = e2e
         print(json.dumps(out), flush=True)
     D.close()
     return 0

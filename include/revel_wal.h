@@ -144,6 +144,10 @@ int revel_gpu_device_count(int* count);
 /* PCI bus id ("dddd:bb:dd.f") of a visible HIP device: which physical GPU a
  * process drove (bench.py reports it per rank). */
 int revel_gpu_device_pci_bus_id(int device, char* buf, size_t cap);
+/* The compiler that built this library's gfx950 kernels (hipcc's clang
+ * version string) and the offload target: build provenance for bench.py's
+ * JSON line.  Static storage; never NULL. */
+const char* revel_build_info(void);
 /* One context per (thread, device): owns a HIP stream and scratch.  Every
  * GPU entry point binds the context's device for the duration of the call and
  * restores the calling thread's current device before it returns. */

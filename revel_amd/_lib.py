@@ -120,6 +120,7 @@ SIGNATURES = {
     "revel_log_reader_new": (c_int, [c_void_p, c_int, c_uint64, c_void_p, c_size_t, POINTER(c_void_p)]),
     "revel_log_reader_read_record": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
     "revel_gpu_device_pci_bus_id": (c_int, [c_int, c_char_p, c_size_t]),
+    "revel_build_info": (c_char_p, []),
     "revel_log_reader_read_record_into": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_size_t), POINTER(c_int)]),
     "revel_log_reader_last_record_offset": (c_uint64, [c_void_p]),
     "revel_log_reader_free": (None, [c_void_p]),

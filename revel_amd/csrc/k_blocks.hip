@@ -184,3 +184,7 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 }
 
 }  // namespace revel
+
+// Build provenance (revel_wal.h): hipcc's clang, which compiled this file's
+// kernels, and the offload target.
+extern "C" const char* revel_build_info(void) { return "hipcc clang " __clang_version__ "; --offload-arch=gfx950"; }

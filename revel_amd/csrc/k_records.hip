@@ -27,6 +27,10 @@ __device__ __forceinline__ Hdr header_in_window(uint3 w, uint32_t sh) {
 // kListCap headers (list_entry; the walk stops at the
 // first bad header, so only the last entry can be bad) followed by the in-block
 // offset of record kListCap when the block has more records.
+// Entries are stored in pairs (below): the pending even entry is flushed on an
+// odd hop or, at the end, for an odd count <= kListCap -- complete only
+// because kListCap is even (entry kListCap - 1 is always the odd one of a pair).
+static_assert(kListCap % 2 == 0, "paired header-list stores need an even kListCap");
 __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ image, uint64_t nbytes, uint64_t b,
                                                 uint64_t* __restrict__ hlist) {
     const uint64_t base = b * kBlockSize;
@@ -1178,7 +1182,8 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
 
 // Verify (or FRAME: append framing) split by block density, from the
 // per-block record counts.  Production (ROWS): the whole blocks with
-// 1..kListPerBlock records are listed (k_sparse_blocks) and verified by
+// 1..kListPerBlock records are listed (count-sorted: k_scan_order, or
+// launch_block_order) and verified by
 // k_verify_rows; !ROWS = v3 over those blocks (experiments only, with its
 // TQ / R64 / TQ8 load shapes).  Lists: verify = hlist + overflow entries in the
 // result slots (xlist = out, 3 u64 apart); FRAME = framing list.

@@ -34,6 +34,11 @@ def device_count() -> int:
     return n.value
 
 
+def build_info() -> str:
+    """The compiler (and target) that built librevel_wal.so's kernels."""
+    return lib().revel_build_info().decode()
+
+
 def pci_bus_id(device: int) -> str:
     """PCI bus id of a visible HIP device (which physical GPU ran)."""
     buf = ctypes.create_string_buffer(64)

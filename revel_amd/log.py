@@ -65,11 +65,14 @@ class Reader:
             return None
         return ctypes.string_at(p.value, n.value) if n.value else b""
 
-    def read_record_into(self, scratch: bytearray) -> Optional[memoryview]:
+    def read_record_into(self, scratch: bytearray) -> Optional[int]:
         """``read_record(&mut scratch)`` with the reference's ownership
         (log_reader.rs:76): the record is written into ``scratch``, grown
-        when the library reports the bytes it needs; returns a view of the
-        record's bytes in ``scratch``, ``None`` at EOF."""
+        when the library reports the bytes it needs; returns the record's
+        length ``n`` (the record is ``scratch[:n]``, valid until the next
+        call, as the reference's ``Slice<'b>`` borrows the scratch), ``None``
+        at EOF.  No view of ``scratch`` is held between calls, so the scratch
+        may grow on any call."""
         n, eof = c_size_t(), ctypes.c_int()
         while True:
             buf = (ctypes.c_char * len(scratch)).from_buffer(scratch) if len(scratch) else None
@@ -82,7 +85,7 @@ class Reader:
             check(rc)
             if eof.value:
                 return None
-            return memoryview(scratch)[:n.value]
+            return n.value
 
     def last_record_offset(self) -> int:
         return lib().revel_log_reader_last_record_offset(self._h)

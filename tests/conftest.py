@@ -27,6 +27,19 @@ def trace(*a):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run on the MI355X box)")
+    config.addinivalue_line("markers", "experiment: kernel arms of tools/experiments (GPU, `-m experiment` only)")
+
+
+def pytest_collection_modifyitems(config, items):
+    """The experiment arms run only when the marker expression names them:
+    `-m gpu` certifies librevel_wal.so alone, and `-m "not gpu"` (CPU) must
+    not try to load libexperiments.so."""
+    if "experiment" in (config.option.markexpr or ""):
+        return
+    skip = pytest.mark.skip(reason="experiment arm: run with -m experiment on a GPU box")
+    for it in items:
+        if it.get_closest_marker("experiment"):
+            it.add_marker(skip)
 
 
 def _traced(cls, names):

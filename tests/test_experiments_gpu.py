@@ -10,7 +10,9 @@ from conftest import golden_image
 from oracle import oracle_c as oc
 from test_gpu import compare_walk, kat_blocks, run_full, zipf_image
 
-pytestmark = pytest.mark.gpu
+# Not part of the driver's `-m gpu` product suite: run with `-m experiment` on
+# a GPU box after `make -C tools/experiments` (conftest skips them otherwise).
+pytestmark = pytest.mark.experiment
 
 C3_ARMS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 20, 21, 22, 23, 24, 30]
 C2_ARMS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 20, 21, 22]  # 100-106: read-ceiling shapes, no CRC

@@ -166,8 +166,7 @@ def reader_events(rd, into=None, limit=100000):
             continue
         if r is None:
             return out
-        out.append(bytes(r))
-        del r  # a view into the scratch: release it before the scratch grows
+        out.append(bytes(r) if into is None else bytes(into[:r]))
     raise AssertionError("reader did not reach EOF")
 
 
@@ -183,6 +182,19 @@ def test_read_record_into_caller_scratch_every_golden(golden_index, start):
             b = log.Reader(env.CallbackSequentialFile(PySequential(img, chunk)), checksum=False, window_bytes=65536)
             scratch = bytearray(start)
             assert reader_events(a, into=scratch) == reader_events(b), (name, chunk, start)
+
+
+def test_read_record_into_natural_loop_grows_scratch():
+    """The loop a caller writes (`while (n := rd.read_record_into(buf)) is not
+    None`) with records that grow past the scratch mid-loop: the call returns
+    a length, holds no view of the scratch, so growing it never fails."""
+    recs = [b"a" * 3, b"b" * 50000, b"", b"c" * 70000, b"d" * 9]
+    rd = log.Reader(env.MemorySequentialFile(oc.write_image(recs)), checksum=False, window_bytes=65536)
+    buf = bytearray(4)
+    got = []
+    while (n := rd.read_record_into(buf)) is not None:
+        got.append(bytes(buf[:n]))
+    assert got == recs and len(buf) >= 70000
 
 
 def test_read_record_into_short_buffer_keeps_the_record():

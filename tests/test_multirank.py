@@ -102,3 +102,57 @@ def test_bench_refuses_more_gpus_than_visible():
     p = _bench(["--gpus", "4", "--blocks", "64"], devices=2, timeout=60)
     assert p.returncode == 2
     assert "2 gfx950 device(s) visible" in p.stderr
+
+
+def _dry(args, devices, env_extra=None, timeout=300):
+    import json
+    env_extra = env_extra or {}
+    old = {k: os.environ.get(k) for k in env_extra}
+    os.environ.update(env_extra)
+    try:
+        p = _bench(args, devices=devices, timeout=timeout)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_8_dry_run(tmp_path):
+    """The driver's N=8 scaling run, rehearsed on the CPU: 8 ranks (gloo), one
+    `ranks` entry per rank on 8 distinct devices, and the end_to_end leg's
+    shared file: rank 0 checks the free space for 8 x the per-rank part, every
+    rank writes its part at rank x per, all ranks see the whole file.
+    Partitioning: contiguous block-aligned parts (records never cross a block,
+    log_writer.rs:66-76)."""
+    d = _dry(["--gpus", "8", "--dry-run", "--blocks", "64", "--e2e-gib", str(16 * 32768 / 2**30)], devices=8,
+             env_extra={"REVEL_BENCH_DIR": str(tmp_path)})
+    assert d["n_gpus"] == 8 and d["dry_run"]
+    assert [r["rank"] for r in d["ranks"]] == list(range(8))
+    assert sorted(r["device"] for r in d["ranks"]) == list(range(8))
+    assert d["config"]["distinct_devices"] == 8
+    e = d["end_to_end"]
+    assert e["skipped"] is None and e["per_rank_bytes"] == 16 * 32768 and e["file_bytes"] == 8 * 16 * 32768
+    assert [r["file_size_seen"] for r in e["per_rank"]] == [8 * 16 * 32768] * 8
+    assert not os.listdir(tmp_path)  # rank 0 removed the file
+
+
+def test_bench_gpus_8_e2e_skips_together(tmp_path):
+    """Free space short for 8 x the per-rank part, or one rank's write
+    failing: every rank skips the end_to_end leg together and the line is
+    still printed."""
+    big = _dry(["--gpus", "8", "--dry-run", "--blocks", str(1 << 40), "--e2e-gib", "1000000"], devices=8,
+               env_extra={"REVEL_BENCH_DIR": str(tmp_path)})
+    e = big["end_to_end"]
+    assert e["file_bytes"] == 8 * int(1000000 * (1 << 30)) // 32768 * 32768
+    assert "MiB free <" in e["skipped"] and all(r["skipped"] for r in e["per_rank"])
+    bad = _dry(["--gpus", "8", "--dry-run", "--blocks", "64", "--e2e-gib", str(4 * 32768 / 2**30)], devices=8,
+               env_extra={"REVEL_BENCH_DIR": str(tmp_path), "REVEL_BENCH_E2E_FAIL_RANK": "5"})
+    e = bad["end_to_end"]
+    assert e["skipped"] and all(r["skipped"] for r in e["per_rank"])
+    assert not os.listdir(tmp_path)

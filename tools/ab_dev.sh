@@ -1,0 +1,23 @@
+#!/bin/bash
+# A/B of builds of librevel_wal.so on bench.py's device-framed c3 image,
+# alternating processes so that clock drift spreads over all builds:
+#   tools/ab_dev.sh <tag> <rounds> <shape> A.so B.so [C.so ...]
+set -u
+tag=$1; n=$2; shape=$3; shift 3
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$tag/ab_$shape
+mkdir -p "$O"
+for i in $(seq 1 "$n"); do
+  for L in "$@"; do
+    "$R/tools/box_step.sh" 300 "$O/run_${i}_$(basename "$L").log" \
+        python3 "$R/tools/bench_c3dev.py" --lib "$L" --shape "$shape" --iters 7 || exit 99
+  done
+done
+cat "$O"/run_*.log | grep '^{' | python3 -c '
+import json, sys, statistics as st
+rows = [json.loads(l) for l in sys.stdin]
+for lib in sorted({r["lib"] for r in rows}):
+    v = [r["ms_median"] for r in rows if r["lib"] == lib]
+    ok = all(r["bad_records"] == 0 for r in rows if r["lib"] == lib)
+    print(lib, "ms", [round(x, 4) for x in v], "median", round(st.median(v), 4), "ok", ok)
+' | tee "$O/summary.txt"

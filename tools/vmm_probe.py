@@ -1,0 +1,129 @@
+"""Diagnosis of the two round-3 guard-test wrong results (VERDICT r3 #2,
+ADVICE r3): device memory mapped with the HIP virtual-memory API
+(hipMemAddressReserve + hipMemCreate + hipMemMap, tests/test_gpu_guard.py's
+GuardedImage) released while the next image is mapped.
+
+Per iteration: image A is mapped, written by a kernel (synth + frame: pattern
+X), read back; A is released according to the mode; image B (same size) is
+mapped and its VA logged (reused = A's VA); then three views of B are checked:
+  copy   -- host pattern Y copied in (hipMemcpyAsync H2D), read straight back
+            (hipMemcpyAsync D2H): does the copy path see Y?
+  kread  -- the C2 kernel's CRCs of B (a shader READ): Y's CRCs?  (the CRCs of
+            an all-zero block or of X name what it read instead)
+  kwrite -- a kernel writes pattern Z into B, D2H reads it back: Z?
+Modes:
+  nosync -- A unmapped / released / VA freed right after its last synchronous
+            D2H (the round-3 test's GuardedImage.free before 8956d8f)
+  sync   -- hipDeviceSynchronize() first, then the same
+  keepva -- A unmapped + released, its VA range never freed (B gets a new VA)
+  plain  -- B is hipMalloc memory (control)
+
+    python tools/vmm_probe.py [--iters 20] [--modes nosync,sync,keepva,plain]
+
+Prints one JSON line per mode: iterations, VA reuses, mismatches per view and
+what each mismatching read equalled.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--modes", default="nosync,sync,keepva,plain")
+    ap.add_argument("--blocks", type=int, default=2)
+    a = ap.parse_args()
+    from revel_amd import BLOCK_SIZE, gpu
+    from oracle import oracle_c as oc
+    from test_gpu_guard import GuardedImage, _guarded_nbytes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ctx = gpu.GpuContext(0)
+    nbytes = _guarded_nbytes(a.blocks)
+    n = nbytes // BLOCK_SIZE
+    zero_crc = oc.full_block_crcs(np.zeros((1, BLOCK_SIZE), np.uint8))[0]
+    m, ok = ctx.alloc(4 * n), ctx.alloc(n)
+
+    def crcs(buf):
+        ctx.crc_full_blocks(buf, n, m, ok)
+        ctx.sync()
+        return ctx.d2h(m, 4 * n, np.uint32)
+
+    for mode in a.modes.split(","):
+        stats = {"mode": mode, "nbytes": nbytes, "iters": a.iters, "va_reused": 0, "a_mismatch": 0,
+                 "copy_mismatch": 0, "kread_mismatch": 0, "kwrite_mismatch": 0, "kread_saw": [], "copy_saw": [],
+                 "kwrite_saw": [], "events": []}
+        kept = []
+        for i in range(a.iters):
+            sx, sz = 0x1000 + i, 0x9000 + i
+            X = oc.synth_full_blocks(n, seed=sx).reshape(-1)
+            A = GuardedImage(0, nbytes)
+            ctx.synth_full_blocks(A, n, seed=sx)
+            ctx.sync()
+            if not np.array_equal(ctx.d2h(A, nbytes), X):
+                stats["a_mismatch"] += 1
+            va_a = A.va
+            if mode == "sync":
+                hip.hipDeviceSynchronize()
+            if mode == "keepva":
+                A.hip.hipMemUnmap(A.va, A.nbytes)
+                A.hip.hipMemRelease(A.handle)
+                kept.append(A)
+            else:
+                A.release()
+            rng = np.random.default_rng(i)
+            Y = rng.integers(0, 256, nbytes, dtype=np.uint8)
+            B = ctx.alloc(nbytes) if mode == "plain" else GuardedImage(0, nbytes)
+            va_b = B.ptr
+            stats["va_reused"] += int(va_b == va_a)
+            ctx.h2d(B, Y)
+            got = ctx.d2h(B, nbytes)
+            if not np.array_equal(got, Y):
+                stats["copy_mismatch"] += 1
+                stats["copy_saw"].append("X" if np.array_equal(got, X) else
+                                         "zeros" if not got.any() else "other")
+            want = oc.full_block_crcs(Y.reshape(n, BLOCK_SIZE))
+            kr = crcs(B)
+            if not np.array_equal(kr, want):
+                stats["kread_mismatch"] += 1
+                xs = oc.full_block_crcs(X.reshape(n, BLOCK_SIZE))
+                stats["kread_saw"].append("X" if np.array_equal(kr, xs) else
+                                          "zeros" if (kr == zero_crc).all() else "other")
+            ctx.synth_full_blocks(B, n, seed=sz)
+            ctx.sync()
+            got = ctx.d2h(B, nbytes)
+            Z = oc.synth_full_blocks(n, seed=sz).reshape(-1)
+            if not np.array_equal(got, Z):
+                stats["kwrite_mismatch"] += 1
+                stats["kwrite_saw"].append("Y" if np.array_equal(got, Y) else
+                                           "X" if np.array_equal(got, X) else
+                                           "zeros" if not got.any() else "other")
+            stats["events"].append([i, hex(va_a), hex(va_b)])
+            if mode == "sync":
+                hip.hipDeviceSynchronize()
+            if mode == "plain":
+                B.free()
+            elif mode == "keepva":
+                B.hip.hipMemUnmap(B.va, B.nbytes)
+                B.hip.hipMemRelease(B.handle)
+                kept.append(B)
+            else:
+                B.release()
+        hip.hipDeviceSynchronize()
+        for k in kept:
+            k.hip.hipMemAddressFree(k.va, k.reserved)
+        stats["events"] = stats["events"][:6]
+        print(json.dumps(stats), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
