@@ -177,8 +177,10 @@ SIGNATURES = {
     "revel_sharded_replay_free": (None, [c_void_p]),
 }
 
-# exported test hook (not part of the public header): production verify paths
+# exported test hooks (not part of the public header): production verify paths,
+# the C3 pipeline switch (fused walk or count pass)
 EXTRA_SIGNATURES = {
+    "revel_gpu_context_set_c3_walk": (c_int, [c_void_p, c_int]),
     "revel_gpu_verify_records_path": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
                                               c_void_p, c_void_p]),
 }

@@ -75,6 +75,9 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
                 hl[kListCap] = uint64_t(resume);
             }
             ++n;
+#ifdef REVEL_COUNT_MAXHOPS  // timing probe only (wrong counts): the walk's tail cost
+            if (n >= REVEL_COUNT_MAXHOPS) break;
+#endif
             if (!more) break;
             off = next;
             a = an;
@@ -939,6 +942,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 
 #include "verify_dense.inc"
 #include "verify_rows.inc"
+#include "verify_walk.inc"
 
 // Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
@@ -958,6 +962,9 @@ __global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
+#ifndef REVEL_ROWS_DIAG
+#define REVEL_ROWS_DIAG 0  // timing probes only (k_verify_rows' DIAG bits; wrong results when != 0)
+#endif
 
 // ---------------------------------------------------------------------------
 // Device append framing, step 1: scatter fragments (payload bytes + length
@@ -1211,7 +1218,8 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
                 hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, st);
                 if (e != hipSuccess) return e;
             }
-            hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
+            hipLaunchKernelGGL((k_verify_rows<FRAME, ROWS_RING, kRowsThreads, FRAME ? 0 : REVEL_ROWS_DIAG>),
+                               dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + kBlockListAux,
                                d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize,
                                ov ? *ov : OverflowArgs{});
@@ -1293,6 +1301,54 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
 }
 
 uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks) { return block_list(d_hlist, nblocks); }
+
+// ---- the fused pipeline (verify_walk.inc) ----
+bool walk_supported(const void* d_image) { return aligned16(d_image); }
+
+hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                           uint32_t* d_first, uint64_t* d_hlist, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    if (nblocks > 0xFFFFFFFFull / kOrderMul || !aligned16(d_image)) return hipErrorInvalidValue;
+    hipError_t e = ensure_len_tables(di, st);
+    if (e != hipSuccess) return e;
+    uint64_t p = 1;
+    while (p < nblocks) p <<= 1;
+    hipLaunchKernelGGL((k_verify_walk<kRowsRing>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, (uint32_t)(p - 1));
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    uint32_t* aux = block_list(d_hlist, nblocks);
+    const uint64_t ntiles = (nblocks + kWalkTile - 1) / kWalkTile;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, (uint64_t)std::max(1, di.num_cu) * 4));
+    hipLaunchKernelGGL(k_walk_tiles, dim3(grid), dim3(256), 0, st, d_counts, (uint32_t)nblocks, aux + 3);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_walk_scan, dim3(grid), dim3(256), 0, st, d_counts, (uint32_t)nblocks, aux + 3, d_first, aux);
+    return hipGetLastError();
+}
+
+hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                       const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
+                       const uint32_t* d_counts, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    const uint32_t* aux = block_list(d_hlist, nblocks);
+    const OverflowArgs ov{img, nbytes, d_first, d_hlist, d_out};
+    const uint64_t nchunks = (nblocks + kExpandBatch - 1) / kExpandBatch;
+    constexpr uint64_t kWaves = kExpandThreads / 64;
+    const uint64_t grid = std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 8, (nchunks + kWaves - 1) / kWaves));
+    hipLaunchKernelGGL(k_expand_walk, dim3((uint32_t)grid), dim3(kExpandThreads), 0, st, base_offset, d_first, d_out,
+                       d_hlist, d_counts, (uint32_t)nblocks, (uint32_t)(nbytes % kBlockSize), ov, aux);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // dense blocks (the partial tail block too): their lists and the overflow entries in the result slots
+    return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, d_hlist, d_counts,
+                                           reinterpret_cast<const uint64_t*>(d_out),
+                                           (uint32_t)(sizeof(revel_record_result) / 8), st, aux + 1, true);
+}
 
 // The grid of k_count_hist and k_scan_order (they must agree: the same
 // workgroup visits the same chunks in both) and the chunk visiting mask.

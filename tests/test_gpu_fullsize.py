@@ -178,3 +178,35 @@ def test_sharded_replay_256mib_three_contexts():
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_c3_small_shape_vs_oracle(gpu_ctx):
+    """bench.py's c3_small image (64..256-B records, ~200 per block: every
+    block takes the dense path; db_bench-shaped puts through DB::write ->
+    add_record, db.rs:95-120, log_writer.rs:58-97) built by the bench's own
+    helper at 256 MiB: every record against the C oracle's walk, then 500
+    payload flips -> exactly those flagged and the walk equal again."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    img, n, nrec = bench.c3_image(gpu_ctx, "small", 0x5EED0005, 0.25)
+    res = gpu_ctx.verify_image(img, n)
+    assert len(res) == po_fragment_count(bench.c3_sizes("small", 0x5EED0005, int(0.25 * (1 << 30))))
+    assert (res["status"] == 0).all() and len(res) >= nrec
+    host = gpu_ctx.d2h(img, n)
+    assert_walk_equal(res, oc.walk(host, "sse42"))
+    assert_walk_equal(res[res["file_offset"] < 64 * BLOCK_SIZE], oc.walk(host[:64 * BLOCK_SIZE], "bytewise"))
+    # ~200 records per whole block: the dense path, not the rows kernel
+    per_block = np.bincount((res["file_offset"] // BLOCK_SIZE).astype(np.int64))
+    assert np.median(per_block) > 64
+    rng = np.random.default_rng(5)
+    victims = np.sort(rng.choice(np.flatnonzero(res["length"] > 0), 500, replace=False))
+    for v in victims:
+        off = int(res["file_offset"][v]) + 7 + int(rng.integers(0, int(res["length"][v])))
+        host[off] ^= np.uint8(0x08)
+        gpu_ctx.h2d(img, host[off:off + 1], dst_offset=off)
+    res2 = gpu_ctx.verify_image(img, n)
+    assert np.array_equal(np.flatnonzero(res2["status"] != 0), victims)
+    assert_walk_equal(res2, oc.walk(host, "sse42"))
+    img.free()

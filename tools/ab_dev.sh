@@ -1,16 +1,18 @@
 #!/bin/bash
 # A/B of builds of librevel_wal.so on bench.py's device-framed c3 image,
 # alternating processes so that clock drift spreads over all builds:
-#   tools/ab_dev.sh <tag> <rounds> <shape> A.so B.so [C.so ...]
+#   tools/ab_dev.sh <tag> <rounds> <shape> A.so[:walk] B.so[:walk] ...
+# (":1" / ":0" after a library: the fused pipeline on / off in that run)
 set -u
 tag=$1; n=$2; shape=$3; shift 3
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$tag/ab_$shape
 mkdir -p "$O"
 for i in $(seq 1 "$n"); do
-  for L in "$@"; do
-    "$R/tools/box_step.sh" 300 "$O/run_${i}_$(basename "$L").log" \
-        python3 "$R/tools/bench_c3dev.py" --lib "$L" --shape "$shape" --iters 7 || exit 99
+  for spec in "$@"; do
+    L=${spec%%:*}; W=""; [ "$spec" != "$L" ] && W="--walk ${spec##*:}"
+    "$R/tools/box_step.sh" 300 "$O/run_${i}_$(basename "$L")${W// /}.log" \
+        python3 "$R/tools/bench_c3dev.py" --lib "$L" --shape "$shape" --iters 7 $W || exit 99
   done
 done
 cat "$O"/run_*.log | grep '^{' | python3 -c '

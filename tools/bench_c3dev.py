@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--walk", type=int, default=None,
+                    help="1: the fused pipeline (row stream walks the headers), 0: the count pass; default: the "
+                         "context's (REVEL_C3_WALK)")
     a = ap.parse_args()
     if a.lib:
         from revel_amd import _lib
@@ -32,6 +35,8 @@ def main():
     import bench
     from revel_amd import gpu
     ctx = gpu.GpuContext(0)
+    if a.walk is not None:
+        ctx.set_c3_walk(bool(a.walk))
     seed = 0x5EED0003 if a.shape == "zipf" else 0x5EED0005
     img, n, nrec = bench.c3_image(ctx, a.shape, seed, a.gib)
     times = []
@@ -39,7 +44,7 @@ def main():
         t, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters)
         times += t
     ms = float(np.median(times))
-    print(json.dumps({"lib": a.lib or "in-tree", "shape": a.shape, "image_bytes": n, "physical_records": nphys,
+    print(json.dumps({"lib": (a.lib or "in-tree") + ("" if a.walk is None else f":walk{a.walk}"), "shape": a.shape, "image_bytes": n, "physical_records": nphys,
                       "bad_records": bad, "ms_median": round(ms, 4), "ms_min": round(min(times), 4),
                       "ms_all": [round(x, 4) for x in times], "GiB_s": round(n / 2**30 / (ms / 1e3), 1),
                       "alg_GB_s": round((n + 24 * nphys) / (ms / 1e3) / 1e9, 1)}), flush=True)
