@@ -1330,7 +1330,7 @@ hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t n
 
 hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                       const uint32_t* d_counts, hipStream_t st) {
+                       const uint32_t* d_counts, hipStream_t st, bool dense2) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (nblocks == 0) return hipSuccess;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
@@ -1345,6 +1345,14 @@ hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbyte
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // dense blocks (the partial tail block too): their lists and the overflow entries in the result slots
+    if (dense2) {
+        const uint64_t waves = kDenseThreads / 64;
+        const uint32_t g =
+            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
+        hipLaunchKernelGGL(k_verify_records_dense2, dim3(g), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
+                           d_first, d_out, d_hlist, d_counts, aux + 1);
+        return hipGetLastError();
+    }
     return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, d_hlist, d_counts,
                                            reinterpret_cast<const uint64_t*>(d_out),
                                            (uint32_t)(sizeof(revel_record_result) / 8), st, aux + 1, true);

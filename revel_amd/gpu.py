@@ -126,11 +126,13 @@ class GpuContext:
         except Exception:
             pass
 
-    def set_c3_walk(self, on: bool) -> bool:
+    def set_c3_walk(self, on) -> int:
         """Test hook: count_scan_records -> verify_records through the fused
-        pipeline (the row stream walks the headers itself, verify_walk.inc)
-        or through the count pass.  Returns the previous setting."""
-        return bool(lib().revel_gpu_context_set_c3_walk(self._h, 1 if on else 0))
+        pipeline (bit 0: the row stream walks the headers itself,
+        verify_walk.inc) or through the count pass; bit 1: the fused
+        pipeline's dense blocks through k_verify_records_dense2.  Returns the
+        previous setting."""
+        return int(lib().revel_gpu_context_set_c3_walk(self._h, int(on)))
 
     # ---- plumbing ----
     def alloc(self, nbytes: int) -> DeviceBuffer:
@@ -200,7 +202,7 @@ class GpuContext:
         split, 1 = header walk without the count pass's lists, 2 = v3 with the
         lists); variant: an experiment arm of tools/experiments."""
         if isinstance(path, str):
-            prev = self.set_c3_walk(path == "walk")
+            prev = self.set_c3_walk({"walk": 1, "walk2": 3}.get(path, 0))
             try:
                 return self.verify_image(image, nbytes, base_offset, variant=variant)
             finally:

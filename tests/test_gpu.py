@@ -147,7 +147,8 @@ def compare_walk(res, ref):
 
 # Verify paths: "walk" = the C-ABI call sequence revel_gpu_count_scan_records
 # -> revel_gpu_verify_records through the fused pipeline (the row stream walks
-# the headers itself, verify_walk.inc); "count" = the same sequence through the
+# the headers itself, verify_walk.inc; "walk2": its dense blocks through
+# k_verify_records_dense2); "count" = the same sequence through the
 # count pass (its own histogram + k_scan_order build the block list; verify
 # launches k_verify_rows + dense only); then the
 # test hook: 0 = the same density split with the block list built inside
@@ -155,7 +156,7 @@ def compare_walk(res, ref):
 # walking the headers itself (verify without its count pass), 2 = v3 with the
 # header lists (unaligned images).  The experiment arms are checked in
 # test_experiments_gpu.py.
-VERIFY_PATHS = ["walk", "count", 0, 1, 2]
+VERIFY_PATHS = ["walk", "walk2", "count", 0, 1, 2]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--walk", type=int, default=None,
-                    help="1: the fused pipeline (row stream walks the headers), 0: the count pass; default: the "
+                    help="1: the fused pipeline (row stream walks the headers), 3: + dense2, 0: the count pass; default: the "
                          "context's (REVEL_C3_WALK)")
     a = ap.parse_args()
     if a.lib:
@@ -36,7 +36,7 @@ def main():
     from revel_amd import gpu
     ctx = gpu.GpuContext(0)
     if a.walk is not None:
-        ctx.set_c3_walk(bool(a.walk))
+        ctx.set_c3_walk(a.walk)
     seed = 0x5EED0003 if a.shape == "zipf" else 0x5EED0005
     img, n, nrec = bench.c3_image(ctx, a.shape, seed, a.gib)
     times = []
