@@ -962,6 +962,9 @@ __global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
+#ifndef REVEL_WALK_RING
+#define REVEL_WALK_RING 8  // rows in flight per wave in k_verify_walk (8 or 16)
+#endif
 #ifndef REVEL_ROWS_DIAG
 #define REVEL_ROWS_DIAG 0  // timing probes only (k_verify_rows' DIAG bits; wrong results when != 0)
 #endif
@@ -1314,7 +1317,7 @@ hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t n
     if (e != hipSuccess) return e;
     uint64_t p = 1;
     while (p < nblocks) p <<= 1;
-    hipLaunchKernelGGL((k_verify_walk<kRowsRing>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
+    hipLaunchKernelGGL((k_verify_walk<REVEL_WALK_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                        static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, (uint32_t)(p - 1));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
