@@ -16,7 +16,13 @@ Modes:
             D2H (the round-3 test's GuardedImage.free before 8956d8f)
   sync   -- hipDeviceSynchronize() first, then the same
   keepva -- A unmapped + released, its VA range never freed (B gets a new VA)
+  keepphys -- A unmapped, its VA freed (B may reuse it), its physical handle
+            kept until the end (A's pages are neither freed nor wiped)
   plain  -- B is hipMalloc memory (control)
+Reading the views: a stale GPU translation of a reused VA makes kernels see
+A's pages (kread saw "X", or "zeros" once A's pages were wiped on release)
+while the copies see B's; a stale runtime-side VA -> allocation lookup makes
+the COPIES go to A's allocation while kernels see B's pages.
 
     python tools/vmm_probe.py [--iters 20] [--modes nosync,sync,keepva,plain]
 
@@ -39,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--modes", default="nosync,sync,keepva,plain")
+    ap.add_argument("--modes", default="nosync,sync,keepva,keepphys,plain")
     ap.add_argument("--blocks", type=int, default=2)
     a = ap.parse_args()
     from revel_amd import BLOCK_SIZE, gpu
@@ -61,7 +67,7 @@ def main():
         stats = {"mode": mode, "nbytes": nbytes, "iters": a.iters, "va_reused": 0, "a_mismatch": 0,
                  "copy_mismatch": 0, "kread_mismatch": 0, "kwrite_mismatch": 0, "kread_saw": [], "copy_saw": [],
                  "kwrite_saw": [], "events": []}
-        kept = []
+        kept, kept_phys = [], []
         for i in range(a.iters):
             sx, sz = 0x1000 + i, 0x9000 + i
             X = oc.synth_full_blocks(n, seed=sx).reshape(-1)
@@ -77,6 +83,10 @@ def main():
                 A.hip.hipMemUnmap(A.va, A.nbytes)
                 A.hip.hipMemRelease(A.handle)
                 kept.append(A)
+            elif mode == "keepphys":
+                A.hip.hipMemUnmap(A.va, A.nbytes)
+                A.hip.hipMemAddressFree(A.va, A.reserved)
+                kept_phys.append(A)
             else:
                 A.release()
             rng = np.random.default_rng(i)
@@ -120,6 +130,8 @@ def main():
         hip.hipDeviceSynchronize()
         for k in kept:
             k.hip.hipMemAddressFree(k.va, k.reserved)
+        for k in kept_phys:
+            k.hip.hipMemRelease(k.handle)
         stats["events"] = stats["events"][:6]
         print(json.dumps(stats), flush=True)
     ctx.close()
