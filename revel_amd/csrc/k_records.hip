@@ -1312,7 +1312,8 @@ hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t n
                            uint32_t* d_first, uint64_t* d_hlist, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (nblocks == 0) return hipSuccess;
-    if (nblocks > 0xFFFFFFFFull / kOrderMul || !aligned16(d_image)) return hipErrorInvalidValue;
+    // list positions and block indices in 32 bits (the position counter runs to P + W)
+    if (nblocks > (1ull << 30) || !aligned16(d_image)) return hipErrorInvalidValue;
     hipError_t e = ensure_len_tables(di, st);
     if (e != hipSuccess) return e;
     uint64_t p = 1;
