@@ -68,15 +68,28 @@ def main():
                  "copy_mismatch": 0, "kread_mismatch": 0, "kwrite_mismatch": 0, "kread_saw": [], "copy_saw": [],
                  "kwrite_saw": [], "events": []}
         kept, kept_phys = [], []
+        prev = None  # (Z, Y, VA) of the previous iteration's image B
         for i in range(a.iters):
             sx, sz = 0x1000 + i, 0x9000 + i
             X = oc.synth_full_blocks(n, seed=sx).reshape(-1)
             A = GuardedImage(0, nbytes)
             ctx.synth_full_blocks(A, n, seed=sx)
             ctx.sync()
-            if not np.array_equal(ctx.d2h(A, nbytes), X):
-                stats["a_mismatch"] += 1
+            got_a = ctx.d2h(A, nbytes)
             va_a = A.va
+            if not np.array_equal(got_a, X):
+                # which view is wrong: the kernel's (its CRCs of A) or the copy's
+                ka = crcs(A)
+                xs = oc.full_block_crcs(X.reshape(n, BLOCK_SIZE))
+                stats["a_mismatch"] += 1
+                stats.setdefault("a_saw", []).append({
+                    "d2h": "prevZ" if prev is not None and np.array_equal(got_a, prev[0]) else
+                           "prevY" if prev is not None and np.array_equal(got_a, prev[1]) else
+                           "zeros" if not got_a.any() else "other",
+                    "kernel_crcs_of_A": "X" if np.array_equal(ka, xs) else
+                                        "zeros" if (ka == zero_crc).all() else "other",
+                    "va_A": hex(va_a), "va_prev_B": hex(prev[2]) if prev is not None else None,
+                    "A_overlaps_prev_B": bool(prev is not None and prev[2] <= va_a < prev[2] + nbytes)})
             if mode == "sync":
                 hip.hipDeviceSynchronize()
             if mode == "keepva":
@@ -117,6 +130,7 @@ def main():
                                            "X" if np.array_equal(got, X) else
                                            "zeros" if not got.any() else "other")
             stats["events"].append([i, hex(va_a), hex(va_b)])
+            prev = (Z, Y, va_b)
             if mode == "sync":
                 hip.hipDeviceSynchronize()
             if mode == "plain":
@@ -133,6 +147,7 @@ def main():
         for k in kept_phys:
             k.hip.hipMemRelease(k.handle)
         stats["events"] = stats["events"][:6]
+        stats["a_saw"] = stats.get("a_saw", [])[:6]
         print(json.dumps(stats), flush=True)
     ctx.close()
 
