@@ -194,7 +194,6 @@ int revel_gpu_context_new(int device, revel_gpu_context** out) {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->di.num_cu = cu;
     if (const char* w = getenv("REVEL_C3_WALK")) c->c3_walk = atoi(w) != 0;
-    if (const char* w = getenv("REVEL_DENSE2")) c->dense2 = atoi(w) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -370,7 +369,7 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
     if (memo && ctx->hlist_walk) {  // after the fused pass of this image: its results
         HIP_TRY(revel::walk_verify(ctx->di, d_image, nbytes, base_offset, d_first, d_out, ctx->hlist,
-                                   ctx->hlist_counts, pick(ctx, stream), ctx->dense2),
+                                   ctx->hlist_counts, pick(ctx, stream)),
                 "walk verify launch");
         ctx->hlist_image = nullptr;
         return REVEL_OK;
@@ -384,14 +383,12 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
 }
 
 // Test hook (not in the public header): count_scan_records -> verify_records
-// through the fused pipeline (bit 0) or the count pass, the fused pipeline's
-// dense blocks through k_verify_records_dense2 (bit 1); returns the previous
-// setting.  REVEL_C3_WALK / REVEL_DENSE2 set a new context's default.
+// through the fused pipeline (on != 0) or the count pass (0); returns the
+// previous setting.  REVEL_C3_WALK sets a new context's default.
 int revel_gpu_context_set_c3_walk(revel_gpu_context* ctx, int on) {
     if (!ctx) return -1;
-    const int prev = (ctx->c3_walk ? 1 : 0) | (ctx->dense2 ? 2 : 0);
-    ctx->c3_walk = (on & 1) != 0;
-    ctx->dense2 = (on & 2) != 0;
+    const int prev = ctx->c3_walk ? 1 : 0;
+    ctx->c3_walk = on != 0;
     return prev;
 }
 

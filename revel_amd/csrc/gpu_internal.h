@@ -112,7 +112,7 @@ hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t n
                            uint32_t* d_first, uint64_t* d_hlist, hipStream_t st);
 hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                       const uint32_t* d_counts, hipStream_t st, bool dense2 = false);
+                       const uint32_t* d_counts, hipStream_t st);
 
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
                              const uint32_t* d_counts, uint64_t nblocks, uint64_t* d_summary, hipStream_t st);
@@ -260,9 +260,6 @@ struct revel_gpu_context {
     // row stream walks the headers itself; verify_walk.inc).  Default from
     // REVEL_C3_WALK at context creation; revel_gpu_context_set_c3_walk (test hook).
     bool c3_walk = false;
-    // walk_verify's dense blocks through k_verify_records_dense2 (aligned word
-    // streams).  Default from REVEL_DENSE2; revel_gpu_context_set_c3_walk bit 1.
-    bool dense2 = false;
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
     // per-64-block record sums of the last count pass (revel_gpu_count_records),

@@ -92,6 +92,86 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
     return n;
 }
 
+// count_block for the 64 blocks of a wave (block b = lane's), as ONE
+// wave-uniform loop over the hops: a lane whose block is done (or that has
+// none) spends its slot of each hop's load instruction on a line AHEAD of a
+// lane still walking -- the nearest such lane below it, (lane distance) x 128
+// B past that lane's next header window -- so the long chains that end the
+// pass (a few lanes, one dependent miss per record: ~1.5 us a hop)
+// find their next headers in L2.  While most lanes walk, few are idle and the
+// prefetch costs nothing (it is skipped while fewer than 16 lanes are idle).
+// The loads stay inside the target lane's block (the window clamp).
+__device__ __forceinline__ uint32_t count_block_pf(const uint8_t* __restrict__ image, uint64_t nbytes, uint64_t b,
+                                                   bool inb, uint64_t* __restrict__ hlist) {
+    const uint32_t lane = lane_id();
+    const uint64_t base = b * kBlockSize;
+    const uint32_t bl = inb ? (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base) : 0u;
+    const uint8_t* const blk = image + (inb ? base : 0u);
+    uint32_t n = 0;
+    if (inb && bl >= kHeaderSize && bl < 12u) {  // a last block of 7..11 bytes: one header at most
+        const Hdr h = read_header(blk, 0u, bl);
+        hlist[b * kListStride] = list_entry(h);
+        n = 1;
+    }
+    bool walking = inb && bl >= 12u;
+    const uint32_t cap = walking ? bl - 12u : 0u;
+    uint32_t off = 0, a = 0, resume = 0;
+    uint64_t pend = 0;
+    uint64_t* const hl = hlist + (inb ? b : 0u) * kListStride;
+    uint3 w = *reinterpret_cast<const uint3*>(walking ? blk : image);
+    for (uint32_t hop = 0;; ++hop) {  // wave-uniform; every walking lane is at record `hop`
+        Hdr h{0u, 0u, 0u};
+        uint32_t next = 0, an = 0;
+        bool more = false;
+        if (walking) {
+            h = header_in_window(w, off - a);
+            const bool ok = classify(h, off, bl) == REVEL_REC_OK;
+            next = off + kHeaderSize + h.len;  // <= bl when ok
+            more = ok && bl - next >= kHeaderSize;
+            an = min(more ? next & ~3u : 0u, cap);
+        }
+        // the next hop's windows, and the idle lanes' prefetches, in one load instruction
+        const uint64_t mm = __ballot(walking && more);  // lanes that walk on
+        const uint8_t* addr = blk + an;
+        if (__popcll(mm) <= 48 && mm != 0) {  // wave-uniform: >= 16 idle lanes
+            const uint64_t below = mm & ((1ull << lane) - 1ull);
+            const uint32_t t = below ? 63u - (uint32_t)__builtin_clzll(below) : (uint32_t)__builtin_ctzll(mm);
+            const uint32_t k = below ? lane - t : lane + 1u;
+            const uint32_t an_t = (uint32_t)__builtin_amdgcn_ds_bpermute(int(t << 2), int(an));
+            const uint64_t b_t = b - lane + t;
+            const uint32_t bl_t = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - b_t * kBlockSize);
+            const uint32_t pfo = min(an_t + 128u * k, bl_t - 12u);
+            if (!(walking && more)) addr = image + b_t * kBlockSize + pfo;
+        } else if (!(walking && more)) {
+            addr = image;
+        }
+        const uint3 wn = *reinterpret_cast<const uint3*>(addr);
+        if (walking) {
+            // entries in pairs (count_block): hop parity is wave-uniform
+            const uint64_t e = list_entry(h);
+            if (hop < kListCap) {
+                if (hop & 1u) {
+                    const uint64_t pair[2] = {pend, e};
+                    __builtin_memcpy(hl + (hop - 1u), pair, 16);
+                } else {
+                    pend = e;
+                }
+            } else {
+                resume = hop == kListCap ? off : resume;
+                hl[kListCap] = uint64_t(resume);
+            }
+            n = hop + 1u;
+            walking = more;
+            off = next;
+            a = an;
+            w = wn;
+        }
+        if (mm == 0) break;
+    }
+    if (inb && bl >= 12u && (n & 1u) && n <= kListCap) hl[n - 1u] = pend;  // the last entry of an odd count
+    return n;
+}
+
 // One lane per block.  With wsums (one wave per workgroup), wsums[w] = the
 // records of blocks [64 w, 64 w + 64): the first pass of the exclusive scan
 // that follows.  (The replay and shard loaders' count pass; the C-ABI's is
@@ -1181,6 +1261,17 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
     const uint64_t waves = kDenseThreads / 64;
     const uint32_t grid =
         (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
+    if constexpr (!FRAME) {
+        if (lead == 0) {  // verify of a whole image: the aligned-word-stream kernel, every dense block
+            hipLaunchKernelGGL(k_verify_records_dense2, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
+                               base_offset, d_first, d_out, hl, d_counts, dense_whole);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess || vbytes % kBlockSize == 0 || tail_in_rows) return e;
+            hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0,
+                               st, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, 0u);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(k_verify_records_dense<FRAME>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
                        d_first, d_out, lead, hl, d_counts, xl, xs, dense_whole);
     hipError_t e = hipGetLastError();
@@ -1334,7 +1425,7 @@ hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t n
 
 hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                       const uint32_t* d_counts, hipStream_t st, bool dense2) {
+                       const uint32_t* d_counts, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (nblocks == 0) return hipSuccess;
     const uint8_t* img = static_cast<const uint8_t*>(d_image);
@@ -1349,14 +1440,6 @@ hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbyte
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // dense blocks (the partial tail block too): their lists and the overflow entries in the result slots
-    if (dense2) {
-        const uint64_t waves = kDenseThreads / 64;
-        const uint32_t g =
-            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
-        hipLaunchKernelGGL(k_verify_records_dense2, dim3(g), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
-                           d_first, d_out, d_hlist, d_counts, aux + 1);
-        return hipGetLastError();
-    }
     return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, d_hlist, d_counts,
                                            reinterpret_cast<const uint64_t*>(d_out),
                                            (uint32_t)(sizeof(revel_record_result) / 8), st, aux + 1, true);

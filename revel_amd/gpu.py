@@ -128,10 +128,9 @@ class GpuContext:
 
     def set_c3_walk(self, on) -> int:
         """Test hook: count_scan_records -> verify_records through the fused
-        pipeline (bit 0: the row stream walks the headers itself,
-        verify_walk.inc) or through the count pass; bit 1: the fused
-        pipeline's dense blocks through k_verify_records_dense2.  Returns the
-        previous setting."""
+        pipeline (1: the row stream walks the headers itself,
+        verify_walk.inc) or through the count pass (0).  Returns the previous
+        setting."""
         return int(lib().revel_gpu_context_set_c3_walk(self._h, int(on)))
 
     # ---- plumbing ----
@@ -202,7 +201,7 @@ class GpuContext:
         split, 1 = header walk without the count pass's lists, 2 = v3 with the
         lists); variant: an experiment arm of tools/experiments."""
         if isinstance(path, str):
-            prev = self.set_c3_walk({"walk": 1, "walk2": 3}.get(path, 0))
+            prev = self.set_c3_walk(1 if path == "walk" else 0)
             try:
                 return self.verify_image(image, nbytes, base_offset, variant=variant)
             finally:

@@ -147,8 +147,7 @@ def compare_walk(res, ref):
 
 # Verify paths: "walk" = the C-ABI call sequence revel_gpu_count_scan_records
 # -> revel_gpu_verify_records through the fused pipeline (the row stream walks
-# the headers itself, verify_walk.inc; "walk2": its dense blocks through
-# k_verify_records_dense2); "count" = the same sequence through the
+# the headers itself, verify_walk.inc); "count" = the same sequence through the
 # count pass (its own histogram + k_scan_order build the block list; verify
 # launches k_verify_rows + dense only); then the
 # test hook: 0 = the same density split with the block list built inside
@@ -156,7 +155,7 @@ def compare_walk(res, ref):
 # walking the headers itself (verify without its count pass), 2 = v3 with the
 # header lists (unaligned images).  The experiment arms are checked in
 # test_experiments_gpu.py.
-VERIFY_PATHS = ["walk", "walk2", "count", 0, 1, 2]
+VERIFY_PATHS = ["walk", "count", 0, 1, 2]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)
@@ -297,6 +296,26 @@ def test_expander_counts_1_to_64_with_flips(gpu_ctx):
     img = bytes(img) + bytes([0x11, 0x22, 0x33])  # a torn header at the end
     ref = oc.walk(img)
     assert int((ref["status"] == 1).sum()) > 100
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)
+
+
+@pytest.mark.parametrize("plen", [123, 124, 126, 127, 128, 251, 254, 255, 256])
+def test_verify_dense_word_stream_edges(gpu_ctx, plen):
+    """Dense blocks of equal records whose CRC range (type + payload) is a
+    multiple of 32 words or just off it, at every byte alignment of the type
+    byte: the dense kernels' word-stream chunk boundaries (a 32-word record's
+    last word takes a dword of the next chunk), a bit flipped in every 7th."""
+    rng = np.random.default_rng(plen)
+    recs = [rng.integers(0, 256, plen, dtype=np.uint8).tobytes() for _ in range(700)]
+    img = bytearray(oc.write_image(recs))
+    ref = oc.walk(bytes(img))
+    for v in range(0, len(ref), 7):
+        if ref["length"][v]:
+            img[int(ref["file_offset"][v]) + 7 + int(rng.integers(0, int(ref["length"][v])))] ^= 0x10
+    img = bytes(img)
+    ref = oc.walk(img)
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
     for v in VERIFY_PATHS:
         compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--walk", type=int, default=None,
-                    help="1: the fused pipeline (row stream walks the headers), 3: + dense2, 0: the count pass; default: the "
+                    help="1: the fused pipeline (row stream walks the headers), 0: the count pass; default: the "
                          "context's (REVEL_C3_WALK)")
     a = ap.parse_args()
     if a.lib:
