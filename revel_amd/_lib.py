@@ -177,10 +177,8 @@ SIGNATURES = {
     "revel_sharded_replay_free": (None, [c_void_p]),
 }
 
-# exported test hooks (not part of the public header): production verify paths,
-# the C3 pipeline switch (fused walk or count pass)
+# exported test hook (not part of the public header): production verify paths
 EXTRA_SIGNATURES = {
-    "revel_gpu_context_set_c3_walk": (c_int, [c_void_p, c_int]),
     "revel_gpu_verify_records_path": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
                                               c_void_p, c_void_p]),
 }
@@ -193,6 +191,9 @@ EXPERIMENT_SIGNATURES = {
                                                 c_void_p]),
     "revel_x_verify_records_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
                                                c_void_p, c_void_p]),
+    "revel_x_walk_count_scan": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+    "revel_x_walk_verify": (c_int, [c_void_p, c_void_p, c_size_t, c_uint64, c_void_p, c_void_p, c_void_p,
+                                    c_void_p]),
 }
 _xlib = None
 

@@ -193,7 +193,6 @@ int revel_gpu_context_new(int device, revel_gpu_context** out) {
     c->di.device = device;
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->di.num_cu = cu;
-    if (const char* w = getenv("REVEL_C3_WALK")) c->c3_walk = atoi(w) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -301,7 +300,6 @@ int count_pass(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint3
     ctx->hlist_nbytes = nbytes;
     ctx->hlist_counts = d_counts;
     ctx->hlist_list_ready = false;
-    ctx->hlist_walk = false;
     return REVEL_OK;
 }
 }  // namespace
@@ -321,18 +319,6 @@ int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, si
     if (!d_image || !d_counts || !d_first) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     hipStream_t st = pick(ctx, stream);
-    if (ctx->c3_walk && revel::walk_supported(d_image)) {
-        // the fused pipeline: the row stream walks the headers itself (verify_walk.inc)
-        int rc = ensure_hlist(ctx, nblocks);
-        if (rc) return rc;
-        HIP_TRY(revel::walk_count_scan(ctx->di, d_image, nbytes, d_counts, d_first, ctx->hlist, st), "walk launch");
-        ctx->hlist_image = d_image;
-        ctx->hlist_nbytes = nbytes;
-        ctx->hlist_counts = d_counts;
-        ctx->hlist_list_ready = false;
-        ctx->hlist_walk = true;
-        return REVEL_OK;
-    }
     int rc = count_pass(ctx, d_image, nbytes, d_counts, st);
     if (rc) return rc;
     // one launch for the scan (first pass: the count pass's per-64-block sums)
@@ -367,29 +353,12 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
-    if (memo && ctx->hlist_walk) {  // after the fused pass of this image: its results
-        HIP_TRY(revel::walk_verify(ctx->di, d_image, nbytes, base_offset, d_first, d_out, ctx->hlist,
-                                   ctx->hlist_counts, pick(ctx, stream)),
-                "walk verify launch");
-        ctx->hlist_image = nullptr;
-        return REVEL_OK;
-    }
     HIP_TRY(revel::verify_records(ctx->di, d_image, nbytes, base_offset, d_first, d_out, memo ? ctx->hlist : nullptr,
                                   memo ? ctx->hlist_counts : nullptr, pick(ctx, stream),
                                   memo && ctx->hlist_list_ready),
             "verify_records launch");
     ctx->hlist_image = nullptr;  // one count pass -> one verify
     return REVEL_OK;
-}
-
-// Test hook (not in the public header): count_scan_records -> verify_records
-// through the fused pipeline (on != 0) or the count pass (0); returns the
-// previous setting.  REVEL_C3_WALK sets a new context's default.
-int revel_gpu_context_set_c3_walk(revel_gpu_context* ctx, int on) {
-    if (!ctx) return -1;
-    const int prev = ctx->c3_walk ? 1 : 0;
-    ctx->c3_walk = on != 0;
-    return prev;
 }
 
 // Test hook (not in the public header): the production verify paths of

@@ -102,18 +102,6 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
                           const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                           const uint32_t* d_counts, hipStream_t st, bool list_ready = false);
 
-// The fused pipeline (verify_walk.inc): walk_count_scan streams every block
-// (header walk from the rows in registers + prefix captures) and leaves the
-// counts, header lists, captures and the scan (d_first); walk_verify turns
-// the captures into the results (k_expand_walk) and verifies the dense blocks.
-// Images must be 16-B aligned (walk_supported).
-bool walk_supported(const void* d_image);
-hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                           uint32_t* d_first, uint64_t* d_hlist, hipStream_t st);
-hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                       const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                       const uint32_t* d_counts, hipStream_t st);
-
 hipError_t summarize_records(const DeviceInfo& di, const revel_record_result* d_res, const uint32_t* d_first,
                              const uint32_t* d_counts, uint64_t nblocks, uint64_t* d_summary, hipStream_t st);
 hipError_t summarize_blocks(const DeviceInfo& di, const uint8_t* d_ok, uint64_t nblocks, uint64_t base_offset,
@@ -255,11 +243,6 @@ struct revel_gpu_context {
     uint64_t hlist_nbytes = 0;
     const uint32_t* hlist_counts = nullptr;
     bool hlist_list_ready = false;  // the count pass also built verify's block list (count_scan_records)
-    bool hlist_walk = false;        // ... or the fused pass ran (walk_count_scan): verify = walk_verify
-    // count_scan_records -> verify_records through the fused pipeline (the
-    // row stream walks the headers itself; verify_walk.inc).  Default from
-    // REVEL_C3_WALK at context creation; revel_gpu_context_set_c3_walk (test hook).
-    bool c3_walk = false;
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
     // per-64-block record sums of the last count pass (revel_gpu_count_records),

@@ -92,86 +92,6 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
     return n;
 }
 
-// count_block for the 64 blocks of a wave (block b = lane's), as ONE
-// wave-uniform loop over the hops: a lane whose block is done (or that has
-// none) spends its slot of each hop's load instruction on a line AHEAD of a
-// lane still walking -- the nearest such lane below it, (lane distance) x 128
-// B past that lane's next header window -- so the long chains that end the
-// pass (a few lanes, one dependent miss per record: ~1.5 us a hop)
-// find their next headers in L2.  While most lanes walk, few are idle and the
-// prefetch costs nothing (it is skipped while fewer than 16 lanes are idle).
-// The loads stay inside the target lane's block (the window clamp).
-__device__ __forceinline__ uint32_t count_block_pf(const uint8_t* __restrict__ image, uint64_t nbytes, uint64_t b,
-                                                   bool inb, uint64_t* __restrict__ hlist) {
-    const uint32_t lane = lane_id();
-    const uint64_t base = b * kBlockSize;
-    const uint32_t bl = inb ? (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base) : 0u;
-    const uint8_t* const blk = image + (inb ? base : 0u);
-    uint32_t n = 0;
-    if (inb && bl >= kHeaderSize && bl < 12u) {  // a last block of 7..11 bytes: one header at most
-        const Hdr h = read_header(blk, 0u, bl);
-        hlist[b * kListStride] = list_entry(h);
-        n = 1;
-    }
-    bool walking = inb && bl >= 12u;
-    const uint32_t cap = walking ? bl - 12u : 0u;
-    uint32_t off = 0, a = 0, resume = 0;
-    uint64_t pend = 0;
-    uint64_t* const hl = hlist + (inb ? b : 0u) * kListStride;
-    uint3 w = *reinterpret_cast<const uint3*>(walking ? blk : image);
-    for (uint32_t hop = 0;; ++hop) {  // wave-uniform; every walking lane is at record `hop`
-        Hdr h{0u, 0u, 0u};
-        uint32_t next = 0, an = 0;
-        bool more = false;
-        if (walking) {
-            h = header_in_window(w, off - a);
-            const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-            next = off + kHeaderSize + h.len;  // <= bl when ok
-            more = ok && bl - next >= kHeaderSize;
-            an = min(more ? next & ~3u : 0u, cap);
-        }
-        // the next hop's windows, and the idle lanes' prefetches, in one load instruction
-        const uint64_t mm = __ballot(walking && more);  // lanes that walk on
-        const uint8_t* addr = blk + an;
-        if (__popcll(mm) <= 48 && mm != 0) {  // wave-uniform: >= 16 idle lanes
-            const uint64_t below = mm & ((1ull << lane) - 1ull);
-            const uint32_t t = below ? 63u - (uint32_t)__builtin_clzll(below) : (uint32_t)__builtin_ctzll(mm);
-            const uint32_t k = below ? lane - t : lane + 1u;
-            const uint32_t an_t = (uint32_t)__builtin_amdgcn_ds_bpermute(int(t << 2), int(an));
-            const uint64_t b_t = b - lane + t;
-            const uint32_t bl_t = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - b_t * kBlockSize);
-            const uint32_t pfo = min(an_t + 128u * k, bl_t - 12u);
-            if (!(walking && more)) addr = image + b_t * kBlockSize + pfo;
-        } else if (!(walking && more)) {
-            addr = image;
-        }
-        const uint3 wn = *reinterpret_cast<const uint3*>(addr);
-        if (walking) {
-            // entries in pairs (count_block): hop parity is wave-uniform
-            const uint64_t e = list_entry(h);
-            if (hop < kListCap) {
-                if (hop & 1u) {
-                    const uint64_t pair[2] = {pend, e};
-                    __builtin_memcpy(hl + (hop - 1u), pair, 16);
-                } else {
-                    pend = e;
-                }
-            } else {
-                resume = hop == kListCap ? off : resume;
-                hl[kListCap] = uint64_t(resume);
-            }
-            n = hop + 1u;
-            walking = more;
-            off = next;
-            a = an;
-            w = wn;
-        }
-        if (mm == 0) break;
-    }
-    if (inb && bl >= 12u && (n & 1u) && n <= kListCap) hl[n - 1u] = pend;  // the last entry of an odd count
-    return n;
-}
-
 // One lane per block.  With wsums (one wave per workgroup), wsums[w] = the
 // records of blocks [64 w, 64 w + 64): the first pass of the exclusive scan
 // that follows.  (The replay and shard loaders' count pass; the C-ABI's is
@@ -1022,7 +942,6 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 
 #include "verify_dense.inc"
 #include "verify_rows.inc"
-#include "verify_walk.inc"
 
 // Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
@@ -1042,9 +961,6 @@ __global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbyt
     }
 }
 constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
-#ifndef REVEL_WALK_RING
-#define REVEL_WALK_RING 8  // rows in flight per wave in k_verify_walk (8 or 16)
-#endif
 #ifndef REVEL_ROWS_DIAG
 #define REVEL_ROWS_DIAG 0  // timing probes only (k_verify_rows' DIAG bits; wrong results when != 0)
 #endif
@@ -1395,55 +1311,6 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
 }
 
 uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks) { return block_list(d_hlist, nblocks); }
-
-// ---- the fused pipeline (verify_walk.inc) ----
-bool walk_supported(const void* d_image) { return aligned16(d_image); }
-
-hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                           uint32_t* d_first, uint64_t* d_hlist, hipStream_t st) {
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    if (nblocks == 0) return hipSuccess;
-    // list positions and block indices in 32 bits (the position counter runs to P + W)
-    if (nblocks > (1ull << 30) || !aligned16(d_image)) return hipErrorInvalidValue;
-    hipError_t e = ensure_len_tables(di, st);
-    if (e != hipSuccess) return e;
-    uint64_t p = 1;
-    while (p < nblocks) p <<= 1;
-    hipLaunchKernelGGL((k_verify_walk<REVEL_WALK_RING>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, (uint32_t)(p - 1));
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    uint32_t* aux = block_list(d_hlist, nblocks);
-    const uint64_t ntiles = (nblocks + kWalkTile - 1) / kWalkTile;
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, (uint64_t)std::max(1, di.num_cu) * 4));
-    hipLaunchKernelGGL(k_walk_tiles, dim3(grid), dim3(256), 0, st, d_counts, (uint32_t)nblocks, aux + 3);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_walk_scan, dim3(grid), dim3(256), 0, st, d_counts, (uint32_t)nblocks, aux + 3, d_first, aux);
-    return hipGetLastError();
-}
-
-hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                       const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                       const uint32_t* d_counts, hipStream_t st) {
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    if (nblocks == 0) return hipSuccess;
-    const uint8_t* img = static_cast<const uint8_t*>(d_image);
-    const uint32_t* aux = block_list(d_hlist, nblocks);
-    const OverflowArgs ov{img, nbytes, d_first, d_hlist, d_out};
-    const uint64_t nchunks = (nblocks + kExpandBatch - 1) / kExpandBatch;
-    constexpr uint64_t kWaves = kExpandThreads / 64;
-    const uint64_t grid = std::max<uint64_t>(
-        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 8, (nchunks + kWaves - 1) / kWaves));
-    hipLaunchKernelGGL(k_expand_walk, dim3((uint32_t)grid), dim3(kExpandThreads), 0, st, base_offset, d_first, d_out,
-                       d_hlist, d_counts, (uint32_t)nblocks, (uint32_t)(nbytes % kBlockSize), ov, aux);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    // dense blocks (the partial tail block too): their lists and the overflow entries in the result slots
-    return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, d_hlist, d_counts,
-                                           reinterpret_cast<const uint64_t*>(d_out),
-                                           (uint32_t)(sizeof(revel_record_result) / 8), st, aux + 1, true);
-}
 
 // The grid of k_count_hist and k_scan_order (they must agree: the same
 // workgroup visits the same chunks in both) and the chunk visiting mask.

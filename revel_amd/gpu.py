@@ -126,13 +126,6 @@ class GpuContext:
         except Exception:
             pass
 
-    def set_c3_walk(self, on) -> int:
-        """Test hook: count_scan_records -> verify_records through the fused
-        pipeline (1: the row stream walks the headers itself,
-        verify_walk.inc) or through the count pass (0).  Returns the previous
-        setting."""
-        return int(lib().revel_gpu_context_set_c3_walk(self._h, int(on)))
-
     # ---- plumbing ----
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
@@ -194,27 +187,10 @@ class GpuContext:
                      variant: Optional[int] = None, path: Optional[int] = None) -> np.ndarray:
         """Config C3: walk + CRC every physical record of a device-resident
         WAL image.  Returns a structured array (RECORD_DTYPE) in file order.
-        path: None = the C-ABI sequence revel_gpu_count_scan_records ->
-        revel_gpu_verify_records with the context's pipeline, "walk" / "count"
-        = that sequence through the fused pipeline / the count pass; an int =
-        a verify path of the test hook after the count pass (0 = production
-        split, 1 = header walk without the count pass's lists, 2 = v3 with the
-        lists); variant: an experiment arm of tools/experiments."""
-        if isinstance(path, str):
-            prev = self.set_c3_walk(1 if path == "walk" else 0)
-            try:
-                return self.verify_image(image, nbytes, base_offset, variant=variant)
-            finally:
-                self.set_c3_walk(prev)
-        if path is not None or variant is not None:
-            prev = self.set_c3_walk(False)  # the hook's paths follow the count pass
-            try:
-                return self._verify_image(image, nbytes, base_offset, variant, path)
-            finally:
-                self.set_c3_walk(prev)
-        return self._verify_image(image, nbytes, base_offset, variant, path)
-
-    def _verify_image(self, image, nbytes, base_offset, variant, path) -> np.ndarray:
+        path: a verify path of the test hook after the count pass (0 =
+        production split, 1 = header walk without the count pass's lists, 2 =
+        v3 with the lists); variant: an experiment arm of tools/experiments
+        (DESIGN.md 4.2)."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
         if image.nbytes < nbytes:

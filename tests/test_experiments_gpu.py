@@ -43,3 +43,40 @@ def test_c2_crc_arm_vs_oracle(gpu_ctx, variant):
     blocks = np.vstack([blocks, extra])
     got, _ = run_full(gpu_ctx, blocks, variant=variant)
     assert np.array_equal(got, oc.full_block_crcs(blocks))
+
+
+def walk_verify(gpu_ctx, dimg, n):
+    """The fused pipeline (x_verify_walk.inc): revel_x_walk_count_scan ->
+    revel_x_walk_verify, results as verify_image's."""
+    from revel_amd._lib import check, experiments
+    from revel_amd.gpu import RECORD_DTYPE
+    X = experiments()
+    nblocks = (n + 32767) // 32768
+    counts, first = gpu_ctx.alloc(4 * nblocks), gpu_ctx.alloc(4 * nblocks)
+    check(X.revel_x_walk_count_scan(gpu_ctx.handle, dimg.ptr, n, counts.ptr, first.ptr, None))
+    total = int(gpu_ctx.d2h(first, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]) + \
+        int(gpu_ctx.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0])
+    out = gpu_ctx.alloc(max(1, total) * RECORD_DTYPE.itemsize)
+    check(X.revel_x_walk_verify(gpu_ctx.handle, dimg.ptr, n, 0, counts.ptr, first.ptr, out.ptr, None))
+    gpu_ctx.sync()
+    return gpu_ctx.d2h(out, total * RECORD_DTYPE.itemsize, np.uint8).view(RECORD_DTYPE)
+
+
+def test_walk_pipeline_vs_oracle(gpu_ctx, golden_index):
+    """The fused pipeline (measured slower than the count pass, kept as an
+    experiment): golden images, a corrupted Zipf image, dense blocks with
+    records past kListCap, 32-word record streams, a partial tail block."""
+    images = [golden_image(name) for name in golden_index]
+    rng = np.random.default_rng(17)
+    img = bytearray(oc.write_image(zipf_image(rng, 4 << 20)))
+    ref = oc.walk(bytes(img))
+    for v in rng.choice(np.flatnonzero(ref["length"] > 0), 30, replace=False):
+        img[int(ref["file_offset"][v]) + 7 + int(rng.integers(0, int(ref["length"][v])))] ^= 4
+    images.append(bytes(img))
+    images.append(oc.write_image([rng.integers(0, 256, int(s), dtype=np.uint8).tobytes()
+                                  for s in rng.integers(0, 40, 20000)]))
+    images.append(oc.write_image([bytes(127) for _ in range(700)]))
+    images.append(oc.write_image([bytes(64 * 64 + 9) for _ in range(70)])[:-5000])
+    for img in images:
+        dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+        compare_walk(walk_verify(gpu_ctx, dimg, len(img)), oc.walk(img))

@@ -145,17 +145,15 @@ def compare_walk(res, ref):
         assert np.array_equal(res[f].astype(np.uint64), ref[f].astype(np.uint64)), f
 
 
-# Verify paths: "walk" = the C-ABI call sequence revel_gpu_count_scan_records
-# -> revel_gpu_verify_records through the fused pipeline (the row stream walks
-# the headers itself, verify_walk.inc); "count" = the same sequence through the
-# count pass (its own histogram + k_scan_order build the block list; verify
-# launches k_verify_rows + dense only); then the
+# Verify paths: None = the C-ABI call sequence revel_gpu_count_scan_records
+# -> revel_gpu_verify_records (the count pass's own histogram + k_scan_order
+# build the block list; verify launches k_verify_rows + dense only); then the
 # test hook: 0 = the same density split with the block list built inside
 # verify (k_order_hist + k_order_scatter, as after the general scan), 1 = v3
 # walking the headers itself (verify without its count pass), 2 = v3 with the
 # header lists (unaligned images).  The experiment arms are checked in
 # test_experiments_gpu.py.
-VERIFY_PATHS = ["walk", "count", 0, 1, 2]
+VERIFY_PATHS = [None, 0, 1, 2]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)

@@ -164,9 +164,9 @@ def test_dense_last_block_ends_at_unmapped_granule(gpu_ctx):
     g = GuardedImage(0, nbytes)
     try:
         gpu_ctx.h2d(g, np.frombuffer(img, dtype=np.uint8))
-        # the fused pipeline, the count pass (dense blocks: the aligned-word-
-        # stream kernel); production split, header walk, v3 with lists
-        for path in ("walk", "count", 0, 1, 2):
+        # the C-ABI sequence (dense blocks: the aligned-word-stream kernel);
+        # production split, header walk, v3 with lists
+        for path in (None, 0, 1, 2):
             res = gpu_ctx.verify_image(g, nbytes, path=path)
             for f in ("file_offset", "length", "stored_crc", "computed_crc", "status"):
                 assert np.array_equal(res[f], ref[f].astype(res[f].dtype)), (path, f)

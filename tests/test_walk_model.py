@@ -1,4 +1,4 @@
-"""CPU model of the fused C3 pipeline's arithmetic (revel_amd/csrc/verify_walk.inc),
+"""CPU model of the fused C3 pipeline's arithmetic (tools/experiments/x_verify_walk.inc),
 checked against the oracle walk (log_writer.rs:107-111 / log_reader.rs:200-206's
 per-record CRC): it pins what the GPU kernels compute, independent of a GPU.
 
@@ -70,7 +70,7 @@ def sub_row_end(y: int) -> int:
 
 
 def row_header(blk: bytes, K: int, o: int):
-    """verify_walk.inc row_header: lane L = o >> 4 of the raw row at K."""
+    """x_verify_walk.inc row_header: lane L = o >> 4 of the raw row at K."""
     row, nxt = blk[K:K + 1024], blk[K + 1024:K + 2048].ljust(1024, b"\0")
     L, q = o >> 4, o & 15
 

@@ -18,6 +18,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def walk_timed(ctx, img, n, nrec, iters):
+    """bench.c3_verify_timed through the experiment module's fused pipeline."""
+    from revel_amd._lib import check, experiments
+    from revel_amd.gpu import RECORD_DTYPE
+    X = experiments()
+    nblocks = (n + 32767) // 32768
+    counts, first = ctx.alloc(4 * nblocks), ctx.alloc(4 * nblocks)
+    out = ctx.alloc((nrec + 2 * nblocks + 64) * RECORD_DTYPE.itemsize)
+    e0, e1 = ctx.event(), ctx.event()
+    times = []
+    for _ in range(iters):
+        e0.record()
+        check(X.revel_x_walk_count_scan(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
+        check(X.revel_x_walk_verify(ctx.handle, img.ptr, n, 0, counts.ptr, first.ptr, out.ptr, None))
+        e1.record()
+        ctx.sync()
+        times.append(e0.elapsed_ms(e1))
+    nphys = int(ctx.d2h(first, 4 * nblocks, np.uint32)[-1]) + int(ctx.d2h(counts, 4 * nblocks, np.uint32)[-1])
+    res = ctx.d2h(out, nphys * RECORD_DTYPE.itemsize).view(RECORD_DTYPE)
+    return times, nphys, int((res["status"] != 0).sum())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=None)
@@ -25,9 +47,8 @@ def main():
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--rounds", type=int, default=1)
-    ap.add_argument("--walk", type=int, default=None,
-                    help="1: the fused pipeline (row stream walks the headers), 0: the count pass; default: the "
-                         "context's (REVEL_C3_WALK)")
+    ap.add_argument("--walk", type=int, default=0,
+                    help="1: the fused pipeline of tools/experiments (x_verify_walk.inc) instead of the product's")
     a = ap.parse_args()
     if a.lib:
         from revel_amd import _lib
@@ -35,16 +56,14 @@ def main():
     import bench
     from revel_amd import gpu
     ctx = gpu.GpuContext(0)
-    if a.walk is not None:
-        ctx.set_c3_walk(a.walk)
     seed = 0x5EED0003 if a.shape == "zipf" else 0x5EED0005
     img, n, nrec = bench.c3_image(ctx, a.shape, seed, a.gib)
     times = []
     for _ in range(a.rounds):
-        t, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters)
+        t, nphys, bad = (walk_timed if a.walk else bench.c3_verify_timed)(ctx, img, n, nrec, a.iters)
         times += t
     ms = float(np.median(times))
-    print(json.dumps({"lib": (a.lib or "in-tree") + ("" if a.walk is None else f":walk{a.walk}"), "shape": a.shape, "image_bytes": n, "physical_records": nphys,
+    print(json.dumps({"lib": (a.lib or "in-tree") + (":walk" if a.walk else ""), "shape": a.shape, "image_bytes": n, "physical_records": nphys,
                       "bad_records": bad, "ms_median": round(ms, 4), "ms_min": round(min(times), 4),
                       "ms_all": [round(x, 4) for x in times], "GiB_s": round(n / 2**30 / (ms / 1e3), 1),
                       "alg_GB_s": round((n + 24 * nphys) / (ms / 1e3) / 1e9, 1)}), flush=True)

@@ -15,6 +15,7 @@ namespace {
 #include "x_verify_v1.inc"
 #include "x_verify_ring.inc"
 #include "x_verify5.inc"
+#include "x_verify_walk.inc"
 }  // namespace
 
 namespace revel {
@@ -63,6 +64,56 @@ hipError_t launch_rows_shape(const DeviceInfo& di, const uint8_t* img, uint64_t 
     }
     return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, hl, d_counts, xl, xs, st);
 }
+
+// ---- the fused pipeline (x_verify_walk.inc; round 4, measured slower than the count pass) ----
+bool walk_supported(const void* d_image) { return aligned16(d_image); }
+
+hipError_t walk_count_scan(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                           uint32_t* d_first, uint64_t* d_hlist, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    // list positions and block indices in 32 bits (the position counter runs to P + W)
+    if (nblocks > (1ull << 30) || !aligned16(d_image)) return hipErrorInvalidValue;
+    hipError_t e = ensure_len_tables(di, st);
+    if (e != hipSuccess) return e;
+    uint64_t p = 1;
+    while (p < nblocks) p <<= 1;
+    hipLaunchKernelGGL((k_verify_walk<kRowsRing>), dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, (uint32_t)(p - 1));
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    uint32_t* aux = block_list(d_hlist, nblocks);
+    const uint64_t ntiles = (nblocks + kWalkTile - 1) / kWalkTile;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, (uint64_t)std::max(1, di.num_cu) * 4));
+    hipLaunchKernelGGL(k_walk_tiles, dim3(grid), dim3(256), 0, st, d_counts, (uint32_t)nblocks, aux + 3);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_walk_scan, dim3(grid), dim3(256), 0, st, d_counts, (uint32_t)nblocks, aux + 3, d_first, aux);
+    return hipGetLastError();
+}
+
+hipError_t walk_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                       const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
+                       const uint32_t* d_counts, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    const uint32_t* aux = block_list(d_hlist, nblocks);
+    const OverflowArgs ov{img, nbytes, d_first, d_hlist, d_out};
+    const uint64_t nchunks = (nblocks + kExpandBatch - 1) / kExpandBatch;
+    constexpr uint64_t kWaves = kExpandThreads / 64;
+    const uint64_t grid = std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 8, (nchunks + kWaves - 1) / kWaves));
+    hipLaunchKernelGGL(k_expand_walk, dim3((uint32_t)grid), dim3(kExpandThreads), 0, st, base_offset, d_first, d_out,
+                       d_hlist, d_counts, (uint32_t)nblocks, (uint32_t)(nbytes % kBlockSize), ov, aux);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // dense blocks (the partial tail block too): their lists and the overflow entries in the result slots
+    return launch_dense_and_partial<false>(di, img, nbytes, base_offset, d_first, d_out, 0u, d_hlist, d_counts,
+                                           reinterpret_cast<const uint64_t*>(d_out),
+                                           (uint32_t)(sizeof(revel_record_result) / 8), st, aux + 1, true);
+}
+
 
 hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                     const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
@@ -379,4 +430,43 @@ extern "C" __attribute__((visibility("default"))) int revel_x_verify_rows_list(
                        d_list);
     ctx->hlist_image = nullptr;
     return hipGetLastError() == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
+
+// The fused C3 pipeline (x_verify_walk.inc) on a product context: the row
+// stream walks the headers itself (no count pass), then k_expand_walk.  Same
+// contract as revel_gpu_count_scan_records / revel_gpu_verify_records (the
+// second call uses the header lists and captures of the first, for the same
+// image).  Round 4: parity-green, slower than the count pass.
+extern "C" __attribute__((visibility("default"))) int revel_x_walk_count_scan(
+    revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint32_t* d_counts, uint32_t* d_first, void* stream) {
+    if (!ctx || !d_image || !d_counts || !d_first) return REVEL_INVALID_ARGUMENT;
+    if (nbytes == 0) return REVEL_OK;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks > ctx->hlist_cap_blocks) {
+        if (ctx->hlist) (void)hipFree(ctx->hlist);
+        ctx->hlist = nullptr;
+        ctx->hlist_cap_blocks = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->hlist), revel::hlist_words(nblocks) * sizeof(uint64_t)) !=
+            hipSuccess)
+            return REVEL_IO_ERROR;
+        ctx->hlist_cap_blocks = nblocks;
+    }
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = revel::walk_count_scan(ctx->di, d_image, nbytes, d_counts, d_first, ctx->hlist, st);
+    ctx->hlist_image = nullptr;  // the product's verify must not take these lists for a count pass's
+    if (e == hipErrorInvalidValue) return REVEL_INVALID_ARGUMENT;
+    return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
+extern "C" __attribute__((visibility("default"))) int revel_x_walk_verify(
+    revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint64_t base_offset, const uint32_t* d_counts,
+    const uint32_t* d_first, revel_record_result* d_out, void* stream) {
+    if (!ctx || !d_image || !d_counts || !d_first || !d_out) return REVEL_INVALID_ARGUMENT;
+    if (nbytes == 0) return REVEL_OK;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = revel::walk_verify(ctx->di, d_image, nbytes, base_offset, d_first, d_out, ctx->hlist, d_counts, st);
+    return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
 }
