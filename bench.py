@@ -59,7 +59,7 @@ def parse(argv=None):
                     help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
-    ap.add_argument("--c3-small-gib", type=float, default=1.0,
+    ap.add_argument("--c3-small-gib", type=float, default=4.0,
                     help="per-rank device-framed image of 64..256 B records for the c3_small field (0 = skip)")
     ap.add_argument("--share-gpus", action="store_true",
                     help="rehearsal: allow more ranks than GPUs (rank r drives GPU r mod count)")

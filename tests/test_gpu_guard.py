@@ -81,11 +81,20 @@ class GuardedImage:
         self.ptr = self.va
 
     def free(self):
-        """Deferred to the end of the module (release_all): an image released
-        here lets the next test's allocation reuse its physical pages, and one
-        run read the previous test's data through them (lines written by a
-        kernel into memory of this API were not written back before the
-        release, it seems) -- so no physical page is reused within the module."""
+        """Deferred to the end of the module (release_all), so that no VA range
+        is reserved and mapped a second time within the module.  Round 3 saw
+        two wrong results in this file, and round 4 traced them to that reuse
+        (tools/vmm_probe.py, profiles/r4/s3_vmm_probe_stale_translation_box.log;
+        DESIGN.md 4.9): on one box, once ranges of this API had been unmapped,
+        released and reserved again for new physical memory, KERNEL accesses
+        and the runtime's COPIES to the same VA reached different memory (one
+        side through a stale translation), while copies agreed with copies.
+        A kernel write read back by a D2H copy then returns other bytes (the r3
+        D2H after synth_full_blocks), and a kernel reading an H2D-copied image
+        sees other pages (the r3 C2 launch that returned 2931026674 for two
+        blocks: the masked CRC of an all-zero block).  It needed the reuse: no
+        mismatch without it, none on the other boxes, and none ever with
+        hipMalloc memory (the probe's plain mode and every other GPU test)."""
         _LIVE.append(self)
 
     def release(self):
@@ -136,11 +145,9 @@ def test_full_blocks_end_at_unmapped_granule(gpu_ctx):
     its loads stay inside the image."""
     nbytes = _guarded_nbytes(2)
     n = nbytes // BLOCK_SIZE
-    # the blocks come from the host, as in the dense test: one r3 run copied
-    # the 64-KiB guarded range back after a device-side synth and got the
-    # bytes it held before the synth (a D2H copy of virtual-memory-API memory
-    # that did not see lines still dirty in L2, it seems); what this test is
-    # about is the C2 kernel's loads, so no device write precedes a D2H here
+    # the blocks come from the host (the test is about the C2 kernel's loads);
+    # with no VA range reused in this module (GuardedImage.free), the H2D copy
+    # and the kernel see the same pages
     host = oc.synth_full_blocks(n, seed=0x5EED0002)
     g = GuardedImage(0, nbytes)
     try:
