@@ -49,22 +49,13 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
         uint64_t pend = 0;
         uint64_t* const hl = hlist + b * kListStride;
         uint3 w = *reinterpret_cast<const uint3*>(blk);
-#ifdef REVEL_COUNT_PF2  // A/B probe: from hop REVEL_COUNT_PF2 on, a touch of the line after the next window
-        uint32_t pf_prev = 0, pf_acc = 0;
-#endif
         for (;;) {
-#ifdef REVEL_COUNT_PF2
-            pf_acc ^= pf_prev;  // consumed a hop later: the wait for it is the wait for the window load
-#endif
             const Hdr h = header_in_window(w, off - a);
             const bool ok = classify(h, off, bl) == REVEL_REC_OK;
             const uint32_t next = off + kHeaderSize + h.len;  // <= bl when ok
             const bool more = ok && bl - next >= kHeaderSize;
             const uint32_t an = min(more ? next & ~3u : 0u, cap);
             const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
-#ifdef REVEL_COUNT_PF2
-            pf_prev = n >= REVEL_COUNT_PF2 ? *reinterpret_cast<const uint32_t*>(blk + min(an + 128u, cap)) : 0u;
-#endif
             // The lanes still walking all stand at the same hop n (they start
             // together and take one hop per iteration), so n's parity is
             // wave-uniform: entries are stored in pairs (one 16-B store every
@@ -93,9 +84,6 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
             w = wn;
         }
         if ((n & 1u) && n <= kListCap) hl[n - 1u] = pend;  // the last entry of an odd count
-#ifdef REVEL_COUNT_PF2
-        if ((pf_acc ^ pf_prev) == 0x9E3779B9u && n == 0xFFFFu) hl[0] = 0;  // keeps the touches
-#endif
     } else if (bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
         const Hdr h = read_header(blk, 0u, bl);
         hlist[b * kListStride] = list_entry(h);

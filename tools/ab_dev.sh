@@ -20,6 +20,8 @@ import json, sys, statistics as st
 rows = [json.loads(l) for l in sys.stdin]
 for lib in sorted({r["lib"] for r in rows}):
     v = [r["ms_median"] for r in rows if r["lib"] == lib]
+    w = [r["ms_stream"] for r in rows if r["lib"] == lib and r.get("ms_stream")]
     ok = all(r["bad_records"] == 0 for r in rows if r["lib"] == lib)
-    print(lib, "ms", [round(x, 4) for x in v], "median", round(st.median(v), 4), "ok", ok)
+    print(lib, "ms", [round(x, 4) for x in v], "median", round(st.median(v), 4),
+          "stream", [round(x, 4) for x in w], "median", round(st.median(w), 4) if w else None, "ok", ok)
 ' | tee "$O/summary.txt"
