@@ -99,21 +99,10 @@ __device__ __forceinline__ void finish_full_block(uint32_t u0, uint32_t u1, uint
 // counts stay exact.  A chain carries x = U ^ (next word): the four table
 // words and the next data word fold with two 3-input xors.
 // ---------------------------------------------------------------------------
-// kC2Scramble (A/B switch): the wave's k-th block is sigma(gwave + k * nwaves),
-// sigma(i) = i * amul mod nblocks (amul coprime with nblocks, ~0.618 nblocks):
-// the blocks read at the same time lie scattered over the image instead of
-// 4 096 consecutive blocks at the same row offset (32 KiB apart).  Stepping
-// sigma by nwaves is one add and a conditional subtract of nblocks (adelta =
-// nwaves * amul mod nblocks, from the host).
-#ifndef REVEL_C2_SCRAMBLE
-#define REVEL_C2_SCRAMBLE 0
-#endif
-constexpr bool kC2Scramble = REVEL_C2_SCRAMBLE != 0;
 template <int THREADS, bool FRAME>
 __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                           uint32_t* __restrict__ masked_out,
-                                                          uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst,
-                                                          uint64_t amul = 1, uint64_t adelta = 0) {
+                                                          uint8_t* __restrict__ ok_out, uint8_t* __restrict__ frame_dst) {
     __shared__ alignas(16) uint32_t tab[32768];  // 128 KiB: T'' replicated 32x
     __shared__ uint32_t shtab[8 * 1024];  // 32 KiB: inverse-shift tree tables
     fill_gap_tables(tab, c_gap1020);
@@ -132,36 +121,6 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restr
         return ldg4(reinterpret_cast<const uint4*>(lane_base + b * kBlockSize + g * 1024));
     };
     uint4 ring[16];
-    if constexpr (kC2Scramble) {
-        uint64_t b = __builtin_amdgcn_readfirstlane(uint32_t((unsigned __int128)gwave * amul % nblocks));
-#pragma unroll
-        for (int g = 0; g < 16; ++g) ring[g] = row(b, g);
-        for (uint64_t i = gwave; i < nblocks; i += nwaves) {
-            uint64_t bn = b + adelta;
-            bn = bn >= nblocks ? bn - nblocks : bn;
-            if (i + nwaves >= nblocks) bn = b;  // no next block: its prefetch re-reads this one
-            uint32_t u0, u1, u2, u3;
-            uint4 hdr;
-#pragma unroll
-            for (int g = 0; g < 32; ++g) {
-                if (g == 0) {
-                    uint4 c = ring[0];
-                    zero_header_bytes(c, l0, FRAME, &hdr);
-                    u0 = c.x; u1 = c.y; u2 = c.z; u3 = c.w;
-                    ring[0] = row(b, 16);
-                }
-                const uint4 wn = g < 31 ? ring[(g + 1) & 15] : make_uint4(0, 0, 0, 0);
-                u0 = step_x(u0, wn.x, L, tab);
-                u1 = step_x(u1, wn.y, L, tab);
-                u2 = step_x(u2, wn.z, L, tab);
-                u3 = step_x(u3, wn.w, L, tab);
-                if (g < 31) ring[(g + 1) & 15] = g + 17 < 32 ? row(b, g + 17) : row(bn, g + 17 - 32);
-            }
-            finish_full_block<FRAME>(u0, u1, u2, u3, hdr, b, shtab, lane, masked_out, ok_out, frame_dst);
-            b = bn;
-        }
-        return;
-    }
 #pragma unroll
     for (int g = 0; g < 16; ++g) ring[g] = row(gwave, g);
     for (uint64_t b = gwave; b < nblocks; b += nwaves) {
@@ -194,16 +153,8 @@ hipError_t launch_full4(const DeviceInfo& di, const uint8_t* blocks, uint64_t n,
     constexpr int kThreads = 1024;
     const uint64_t wg_needed = (n + kThreads / 64 - 1) / (kThreads / 64);
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, wg_needed));
-    uint64_t amul = 1, adelta = 0;
-    if (kC2Scramble && n > 1) {
-        amul = (uint64_t)(0.6180339887498949 * double(n)) | 1u;
-        auto gcd = [](uint64_t a, uint64_t b) { while (b) { const uint64_t t = a % b; a = b; b = t; } return a; };
-        while (gcd(amul, n) != 1) amul += 2;
-        amul %= n;
-        adelta = (uint64_t)((unsigned __int128)(grid * (kThreads / 64)) * amul % n);
-    }
     hipLaunchKernelGGL((k_full_blocks4<kThreads, FRAME>), dim3((uint32_t)grid), dim3(kThreads), 0, st, blocks, n,
-                       masked, ok, frame_dst, amul, adelta);
+                       masked, ok, frame_dst);
     return hipGetLastError();
 }
 
