@@ -210,3 +210,41 @@ def test_c3_small_shape_vs_oracle(gpu_ctx):
     assert np.array_equal(np.flatnonzero(res2["status"] != 0), victims)
     assert_walk_equal(res2, oc.walk(host, "sse42"))
     img.free()
+
+
+def test_dense_batches_across_blocks_far_apart(gpu_ctx):
+    """The dense kernel packs a wave's 64-record batches across its dense
+    blocks only while they lie < kDensePackSpan (65 532) blocks apart (its
+    buffer offsets stay in 31 bits).  A 2.2 GB image of full-type blocks with
+    two dense blocks of 306 records (past the 256-entry header list: the
+    overflow entries too) 69 632 blocks apart -- wave 0's consecutive dense
+    blocks when the dense grid has 4 096 waves (256 CUs), else still two
+    dense blocks far apart -- plus a third 4 096 blocks after the first (packed
+    with it): every record against the C oracle's walk."""
+    nb = 69633
+    d = gpu_ctx.alloc(nb * BLOCK_SIZE)
+    gpu_ctx.synth_full_blocks(d, nb, seed=0x5EED0009)
+    rng = np.random.default_rng(9)
+    for b in (0, 4096, nb - 1):
+        recs = [rng.integers(0, 256, 100, dtype=np.uint8).tobytes() for _ in range(305)]
+        recs.append(rng.integers(0, 256, 126, dtype=np.uint8).tobytes())
+        blk = np.frombuffer(oc.write_image(recs), dtype=np.uint8)
+        assert len(blk) == BLOCK_SIZE  # 305 * 107 + 133: the block exactly full
+        gpu_ctx.h2d(d, blk, dst_offset=b * BLOCK_SIZE)
+    gpu_ctx.sync()
+    n = nb * BLOCK_SIZE
+    res = gpu_ctx.verify_image(d, n)
+    host = gpu_ctx.d2h(d, n)
+    ref = oc.walk(host, "sse42")
+    assert len(ref) == nb - 3 + 3 * 306
+    assert_walk_equal(res, ref)
+    assert (res["status"] == 0).all()
+    # a flipped payload byte in each dense block's last record is found
+    for b in (0, nb - 1):
+        host_off = b * BLOCK_SIZE + BLOCK_SIZE - 1
+        byte = host[host_off:host_off + 1] ^ np.uint8(0x40)
+        gpu_ctx.h2d(d, byte, dst_offset=host_off)
+    res2 = gpu_ctx.verify_image(d, n)
+    bad = np.flatnonzero(res2["status"] != 0)
+    assert len(bad) == 2 and (res2["file_offset"][bad] // BLOCK_SIZE).tolist() == [0, nb - 1]
+    d.free()
