@@ -99,6 +99,9 @@ __device__ __forceinline__ void finish_full_block(uint32_t u0, uint32_t u1, uint
 // counts stay exact.  A chain carries x = U ^ (next word): the four table
 // words and the next data word fold with two 3-input xors.
 // ---------------------------------------------------------------------------
+#ifdef REVEL_C2_WAVETIME
+__device__ uint64_t g_c2_wavetime[3 * 65536];
+#endif
 template <int THREADS, bool FRAME>
 __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                           uint32_t* __restrict__ masked_out,
@@ -115,6 +118,9 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restr
     const uint64_t gwave = blockIdx.x * waves_per_wg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nwaves = gridDim.x * waves_per_wg;
     if (gwave >= nblocks) return;
+#ifdef REVEL_C2_WAVETIME  // timing probe: each wave's start / end (s_memrealtime, 100 MHz)
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint8_t* lane_base = blocks + lane * 16u;
     auto row = [&](uint64_t b, int g) {
         b = b < nblocks ? b : nblocks - 1;
@@ -145,6 +151,13 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restr
         }
         finish_full_block<FRAME>(u0, u1, u2, u3, hdr, b, shtab, lane, masked_out, ok_out, frame_dst);
     }
+#ifdef REVEL_C2_WAVETIME
+    if (lane == 0 && gwave < 65536u) {
+        g_c2_wavetime[3u * gwave] = t_start;
+        g_c2_wavetime[3u * gwave + 1u] = __builtin_amdgcn_s_memrealtime();
+        g_c2_wavetime[3u * gwave + 2u] = (nblocks - gwave + nwaves - 1u) / nwaves;
+    }
+#endif
 }
 
 template <bool FRAME>
@@ -188,3 +201,10 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 // Build provenance (revel_wal.h): hipcc's clang, which compiled this file's
 // kernels, and the offload target.
 extern "C" const char* revel_build_info(void) { return "hipcc clang " __clang_version__ "; --offload-arch=gfx950"; }
+
+#ifdef REVEL_C2_WAVETIME
+// timing probe builds only: k_full_blocks4's per-wave start / end times of its last launch
+extern "C" int revel_debug_c2_wavetime(uint64_t* host, uint64_t n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_c2_wavetime), n * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -1224,6 +1224,10 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
     if (b_hi > b_lo) {
         if constexpr (ROWS) {
             // qualifying blocks listed first, most records first (block_order)
+            // k_verify_rows' per-workgroup item counters: the block order's
+            // histogram rows (aux[3..], dead once the list is built; each
+            // workgroup zeroes its own at start)
+            uint32_t* const cursor = d_blist + 3;
             if (!list_ready) {
                 hipError_t e = launch_block_order(di, d_counts, (uint32_t)b_lo, (uint32_t)b_hi, d_blist, st);
                 if (e != hipSuccess) return e;
@@ -1232,7 +1236,7 @@ static hipError_t launch_verify_split(const DeviceInfo& di, const uint8_t* img, 
                                dim3((uint32_t)std::max(1, di.num_cu)), dim3(kRowsThreads), 0, st,
                                img, base_offset, d_first, d_out, lead, hl, d_counts, xl, d_blist + kBlockListAux,
                                d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize,
-                               ov ? *ov : OverflowArgs{});
+                               ov ? *ov : OverflowArgs{}, kRowsDyn ? cursor : nullptr);
             dense_whole = d_blist + 1;
             if constexpr (!FRAME) {
                 hipError_t e = launch_expand_rows(di, base_offset, lead, d_first, d_out, hl, d_counts, (uint32_t)b_lo,
@@ -1398,3 +1402,12 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
 }
 
 }  // namespace revel
+
+#ifdef REVEL_ROWS_WAVETIME
+// timing probe builds only (tools/rows_wavetime.py): k_verify_rows' per-wave
+// start / end times and block counts of its last launch
+extern "C" int revel_debug_rows_wavetime(uint64_t* host, uint64_t n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rows_wavetime), n * sizeof(uint64_t), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
