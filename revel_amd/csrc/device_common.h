@@ -203,6 +203,22 @@ __device__ void fill_tables(uint32_t* tab) {
     }
 }
 
+
+// Wave priority rotation (s_setprio, an immediate 0..3): the SIMD issues the
+// highest-priority ready wave first, then the oldest, so with equal
+// priorities a workgroup's older waves run ahead of its younger ones (the C2
+// kernel's waves finished at 2.6 / 3.5 / 4.4 / 4.9 ms of 5.2 by age rank,
+// profiles/r4/s20_*).  rotate_prio(r) sets priority r & 3; a wave calling it
+// with (its age rank + blocks done) takes every priority in turn.
+__device__ __forceinline__ void rotate_prio(uint32_t r) {
+    switch (__builtin_amdgcn_readfirstlane(r) & 3u) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 struct LaneConst {
     uint32_t lc0, lc1;
 };
