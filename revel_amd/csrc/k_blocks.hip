@@ -102,10 +102,6 @@ __device__ __forceinline__ void finish_full_block(uint32_t u0, uint32_t u1, uint
 #ifdef REVEL_C2_WAVETIME
 __device__ uint64_t g_c2_wavetime[3 * 65536];
 #endif
-#ifndef REVEL_C2_XCD
-#define REVEL_C2_XCD 0
-#endif
-constexpr int kC2Xcd = REVEL_C2_XCD;
 template <int THREADS, bool FRAME>
 __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restrict__ blocks, uint64_t nblocks,
                                                           uint32_t* __restrict__ masked_out,
@@ -131,26 +127,9 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restr
         return ldg4(reinterpret_cast<const uint4*>(lane_base + b * kBlockSize + g * 1024));
     };
     uint4 ring[16];
-    // kC2Xcd (A/B switch, REVEL_C2_XCD = per-mille): the even-index workgroups
-    // (XCDs 0, 2, 4, 6 under the round-robin dispatch) take blocks [0, ne) and
-    // the odd ones [ne, n), ne = n (1000 + REVEL_C2_XCD) / 2000, each half
-    // strided over its own waves (the odd XCDs' waves ended ~10 % later,
-    // profiles/r4/s20_*)
-    uint64_t lo = 0, hi = nblocks, gw = gwave, stride = nwaves;
-    if constexpr (kC2Xcd != 0) {
-        if ((gridDim.x & 1u) == 0 && nblocks >= 2u * nwaves) {
-            const uint64_t ne = nblocks * uint64_t(1000 + kC2Xcd) / 2000u;
-            const bool even = (blockIdx.x & 1u) == 0;
-            lo = even ? 0 : ne;
-            hi = even ? ne : nblocks;
-            stride = nwaves / 2;
-            gw = lo + (blockIdx.x >> 1) * waves_per_wg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            if (gw >= hi) return;
-        }
-    }
 #pragma unroll
-    for (int g = 0; g < 16; ++g) ring[g] = row(gw, g);
-    for (uint64_t b = gw; b < hi; b += stride) {
+    for (int g = 0; g < 16; ++g) ring[g] = row(gwave, g);
+    for (uint64_t b = gwave; b < nblocks; b += nwaves) {
         uint32_t u0, u1, u2, u3;
         uint4 hdr;
 #pragma unroll
@@ -168,7 +147,7 @@ __global__ __launch_bounds__(THREADS) void k_full_blocks4(const uint8_t* __restr
             u2 = step_x(u2, wn.z, L, tab);
             u3 = step_x(u3, wn.w, L, tab);
             // row g + 1 has left its slot: refill with row g + 17
-            if (g < 31) ring[(g + 1) & 15] = g + 17 < 32 ? row(b, g + 17) : row(b + stride, g + 17 - 32);
+            if (g < 31) ring[(g + 1) & 15] = g + 17 < 32 ? row(b, g + 17) : row(b + nwaves, g + 17 - 32);
         }
         finish_full_block<FRAME>(u0, u1, u2, u3, hdr, b, shtab, lane, masked_out, ok_out, frame_dst);
     }

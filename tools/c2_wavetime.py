@@ -47,6 +47,7 @@ def main():
                       "end_us_p0_p10_p50_p90_max": [round(float(np.percentile(e, q)), 1) for q in (0, 10, 50, 90, 100)],
                       "end_us_by_wave_slot_median": [round(float(np.median(e[slot == k])), 1) for k in range(16)],
                       "end_us_by_xcd_median": [round(float(np.median(e[(wg % 8) == x])), 1) for x in range(8)],
+                      "end_us_by_xcd_max": [round(float(np.max(e[(wg % 8) == x])), 1) for x in range(8)],
                       "tail_us_max_minus_p50": round(float(e.max() - np.median(e)), 1)}), flush=True)
     ctx.close()
 
