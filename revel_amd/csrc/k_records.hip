@@ -960,7 +960,10 @@ __global__ void k_list_overflow(const uint8_t* __restrict__ image, uint64_t nbyt
         if (n > kListCap) list_overflow_block(ov, b, n);
     }
 }
-constexpr int kRowsRing = 8;  // rows in flight per wave in k_verify_rows
+#ifndef REVEL_ROWS_RING
+#define REVEL_ROWS_RING 8
+#endif
+constexpr int kRowsRing = REVEL_ROWS_RING;  // rows in flight per wave in k_verify_rows (8 or 16)
 #ifndef REVEL_ROWS_DIAG
 #define REVEL_ROWS_DIAG 0  // timing probes only (k_verify_rows' DIAG bits; wrong results when != 0)
 #endif
