@@ -248,3 +248,22 @@ def test_dense_batches_across_blocks_far_apart(gpu_ctx):
     bad = np.flatnonzero(res2["status"] != 0)
     assert len(bad) == 2 and (res2["file_offset"][bad] // BLOCK_SIZE).tolist() == [0, nb - 1]
     d.free()
+
+
+@pytest.mark.parametrize("shape", ["zipf", "small"])
+def test_bench_c3_legs_report_both_timings(gpu_ctx, shape, monkeypatch):
+    """bench.py's c3 / c3_small legs on a 64 MiB image (single process): the
+    steady-state `ms` (calls queued back to back) and the isolated per-call
+    median are both reported, every record verifies, and the rate is the
+    image over the steady-state time."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    r = bench.c3_records(gpu_ctx, bench.Dist(), 1 / 16, iters=3, shape=shape)
+    assert r["bad_records"] == 0 and r["physical_records_rank0"] > 0
+    assert r["ms"] > 0 and r["ms_isolated"] > 0
+    assert abs(r["value"] - r["per_rank_bytes"] / 2**30 / (r["ms"] / 1e3)) <= 0.05 * r["value"]
+    assert "back to back" in r["timing"]
