@@ -609,10 +609,16 @@ def main(argv=None):
 
     if D.rank == 0:
         out = result_line(args, D, ranks, value=round(value, 1), ms=round(wall / args.steps * 1e3, 4))
+        binfo = gpu.build_info()
         out["config"].update({"kernel_variant": "production" if args.variant is None else args.variant,
                               "all_verify_flags_ok": all_ok,
                               "library_sha256": library_sha256(),   # which binary ran (build provenance)
-                              "build_info": gpu.build_info()})
+                              "build_info": binfo,
+                              # XFLAGS builds (timing probes, A/B switches) are not the product
+                              "diagnostic_build": "XFLAGS:" in binfo})
+        if "XFLAGS:" in binfo:
+            print(f"bench.py: WARNING: librevel_wal.so is a variant build ({binfo}); not a product measurement",
+                  file=sys.stderr, flush=True)
         out["roofline"] = {
             "bound": "hbm",
             "achieved": round(achieved, 1),

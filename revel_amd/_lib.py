@@ -177,10 +177,13 @@ SIGNATURES = {
     "revel_sharded_replay_free": (None, [c_void_p]),
 }
 
-# exported test hook (not part of the public header): production verify paths
+# exported test hooks (not part of the public header): the verify paths, the u32 record-index
+# guard on a synthetic counts array, the one-pass / two-read A/B switch
 EXTRA_SIGNATURES = {
     "revel_gpu_verify_records_path": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
                                               c_void_p, c_void_p]),
+    "revel_debug_check_record_index": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "revel_debug_set_fused": (c_int, [c_int]),
 }
 
 # tools/experiments/libexperiments.so: kernel variants kept for the record

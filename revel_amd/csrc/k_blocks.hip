@@ -200,7 +200,13 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 
 // Build provenance (revel_wal.h): hipcc's clang, which compiled this file's
 // kernels, and the offload target.
-extern "C" const char* revel_build_info(void) { return "hipcc clang " __clang_version__ "; --offload-arch=gfx950"; }
+// REVEL_BUILD_FLAGS: the Makefile's "--offload-arch=$(ARCH) $(XFLAGS)", so a
+// variant build (timing probes, A/B switches: wrong results or other kernels)
+// names its flags wherever bench.py prints the provenance.
+#ifndef REVEL_BUILD_FLAGS
+#define REVEL_BUILD_FLAGS "(flags unknown: built outside revel_amd/csrc/Makefile)"
+#endif
+extern "C" const char* revel_build_info(void) { return "hipcc clang " __clang_version__ "; " REVEL_BUILD_FLAGS; }
 
 #ifdef REVEL_C2_WAVETIME
 // timing probe builds only: k_full_blocks4's per-wave start / end times of its last launch

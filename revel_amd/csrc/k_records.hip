@@ -584,20 +584,25 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 
 // ---------------------------------------------------------------------------
 // The blocks b0, b0 + step, ... < hi of one wave whose record count is above
-// kListPerBlock (DENSE) or at most kListPerBlock (!DENSE): one vector load of
+// MINN (DENSE) or at most MINN (!DENSE): one vector load of
 // 64 candidates' counts, then one set bit of the ballot per block.  Every
 // member is wave-uniform.
 // ---------------------------------------------------------------------------
-template <bool DENSE>
+// MARK (one-pass path, verify_fused.inc): a block whose header list slot
+// kListCap holds kCapMarker qualifies too (walked and listed only, <= MINN records).
+constexpr uint64_t kCapMarker = ~0ull;
+template <bool DENSE, uint32_t MINN = kListPerBlock, bool MARK = false>
 struct BlockSeq {
     uint32_t scan;  // first candidate not yet in mask (block indices fit 32 bits: 128 TiB images)
     uint64_t mask;  // qualifying blocks among scan - 64 step .. scan - step
     __device__ explicit BlockSeq(uint64_t b0) : scan((uint32_t)b0), mask(0) {}
-    __device__ uint64_t next(const uint32_t* __restrict__ counts, uint64_t step, uint64_t hi) {
+    __device__ uint64_t next(const uint32_t* __restrict__ counts, uint64_t step, uint64_t hi,
+                             const uint64_t* __restrict__ hlist = nullptr) {
         while (mask == 0) {
             if (scan >= hi) return hi;
             const uint64_t c = scan + uint64_t(lane_id()) * step;
-            const bool sel = c < hi && ((counts[c] > kListPerBlock) == DENSE);
+            bool sel = c < hi && ((counts[c] > MINN) == DENSE);
+            if constexpr (MARK) sel = sel || (c < hi && hlist[c * kListStride + kListCap] == kCapMarker);
             mask = __ballot(sel);
             scan += (uint32_t)(64u * step);
         }
@@ -942,6 +947,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 
 #include "verify_dense.inc"
 #include "verify_rows.inc"
+#include "verify_fused.inc"
 
 // Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
@@ -1182,7 +1188,7 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
         (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     if constexpr (!FRAME) {
         if (lead == 0) {  // verify of a whole image: the aligned-word-stream kernel, every dense block
-            hipLaunchKernelGGL(k_verify_records_dense2, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
+            hipLaunchKernelGGL(k_verify_records_dense2<>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
                                base_offset, d_first, d_out, hl, d_counts, dense_whole);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess || vbytes % kBlockSize == 0 || tail_in_rows) return e;
@@ -1319,6 +1325,94 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
 
 uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks) { return block_list(d_hlist, nblocks); }
 
+// ---- the one-pass count + checksum path (verify_fused.inc) ----
+bool fused_capable(const void* d_image) { return aligned16(d_image); }
+
+hipError_t fused_count(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    hipError_t e = ensure_len_tables(di, st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(d_fb, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    // one workgroup per CU (the 128 KiB tables); waves loop over their blocks
+    const uint64_t grid = std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu), (nblocks + kFusedWaves - 1) / kFusedWaves));
+    hipLaunchKernelGGL(k_walk_verify, dim3((uint32_t)grid), dim3(kFusedThreads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_fb);
+    return hipGetLastError();
+}
+
+__global__ void k_list_overflow_gated(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                      const uint32_t* __restrict__ counts, const uint32_t* __restrict__ first,
+                                      const uint64_t* __restrict__ hlist, revel_record_result* __restrict__ out,
+                                      const uint32_t* __restrict__ fb) {
+    if (__builtin_amdgcn_readfirstlane(*fb) == 0u) return;  // no block past kListCap records
+    const OverflowArgs ov{image, nbytes, first, hlist, out};
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t n = counts[b];
+        if (n > kListCap) list_overflow_block(ov, b, n);
+    }
+}
+
+hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
+                        const uint32_t* d_counts, const uint32_t* d_fb, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    // blocks with more than kListCap records: their entries past 256 into their result slots,
+    // then k_verify_records_dense2 over exactly those blocks (both leave at once when fb[0] == 0)
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 4, (nblocks + 255) / 256));
+    hipLaunchKernelGGL(k_list_overflow_gated, dim3((uint32_t)g), dim3(256), 0, st, img, nbytes, d_counts, d_first,
+                       d_hlist, d_out, d_fb);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t nchunks = (nblocks + kExpandBatch - 1) / kExpandBatch;
+    constexpr uint64_t kWaves = kExpandThreads / 64;
+    const uint64_t grid = std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 8, (nchunks + kWaves - 1) / kWaves));
+    hipLaunchKernelGGL(k_expand_fused, dim3((uint32_t)grid), dim3(kExpandThreads), 0, st, img, nbytes, base_offset,
+                       d_first, d_out, d_hlist, d_counts);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t dwaves = kDenseThreads / 64;
+    const uint32_t dgrid =
+        (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + dwaves - 1) / dwaves));
+    hipLaunchKernelGGL((k_verify_records_dense2<kFusedCap, true>), dim3(dgrid), dim3(kDenseThreads), 0, st, img, nbytes,
+                       base_offset, d_first, d_out, d_hlist, d_counts, d_fb);
+    return hipGetLastError();
+}
+
+// Sum of the per-block counts in 64 bits (the u32 record-index guard).
+__global__ void k_sum_counts(const uint32_t* __restrict__ counts, uint64_t n, unsigned long long* __restrict__ total) {
+    unsigned long long s = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        s += counts[i];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (lane_id() == 0 && s) atomicAdd(total, s);
+}
+
+hipError_t total_records(const DeviceInfo& di, const uint32_t* d_counts, uint64_t nblocks,
+                         unsigned long long* d_total, uint64_t* total, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(d_total, 0, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 4, (nblocks + 255) / 256));
+    hipLaunchKernelGGL(k_sum_counts, dim3((uint32_t)grid), dim3(256), 0, st, d_counts, nblocks, d_total);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    unsigned long long h = 0;
+    e = hipMemcpyAsync(&h, d_total, sizeof h, hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(st);
+    *total = h;
+    return e;
+}
+
 // The grid of k_count_hist and k_scan_order (they must agree: the same
 // workgroup visits the same chunks in both) and the chunk visiting mask.
 static void count_grid(const DeviceInfo& di, uint64_t nblocks, uint32_t* grid, uint32_t* cmask) {
@@ -1406,6 +1500,17 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
 
 }  // namespace revel
 
+#ifdef REVEL_FUSED_PHASES
+// timing probe builds only (tools/fused_phases.py): k_walk_verify's summed
+// cycles per phase (reset = 1 zeroes them first, no copy)
+extern "C" int revel_debug_fused_phases(uint64_t* host, int reset) {
+    if (reset) {
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fused_phase), z, sizeof z, 0, hipMemcpyHostToDevice);
+    }
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_phase), 8 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
+}
+#endif
 #ifdef REVEL_ROWS_WAVETIME
 // timing probe builds only (tools/rows_wavetime.py): k_verify_rows' per-wave
 // start / end times and block counts of its last launch

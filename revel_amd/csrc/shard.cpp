@@ -333,6 +333,17 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
             }
         } evfree{k0, k1};
         TRY(revel::exclusive_scan_u32(ctx->di, s->d_counts, s->d_first, nblocks, s->d_scan, comp), "scan");
+        if (nblocks > revel::kNoWrapBlocks) {  // record indices are u32: a shard of 2^32 records or more is refused
+            uint64_t total = 0;
+            TRY(revel::total_records(ctx->di, s->d_counts, nblocks, reinterpret_cast<unsigned long long*>(s->d_sum),
+                                     &total, comp),
+                "total_records");
+            if (total > 0xFFFFFFFFull)
+                return set_error(REVEL_INVALID_ARGUMENT,
+                                 "shard of %llu blocks holds %llu physical records: record indices are u32, load at "
+                                 "most 4294967295 records per shard (use more shards)",
+                                 (unsigned long long)nblocks, (unsigned long long)total);
+        }
         uint32_t tail[2] = {0, 0};
         TRY(hipMemcpyAsync(&tail[0], s->d_first + nblocks - 1, 4, hipMemcpyDeviceToHost, comp), "hipMemcpyAsync");
         TRY(hipMemcpyAsync(&tail[1], s->d_counts + nblocks - 1, 4, hipMemcpyDeviceToHost, comp), "hipMemcpyAsync");

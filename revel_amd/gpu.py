@@ -189,7 +189,8 @@ class GpuContext:
         WAL image.  Returns a structured array (RECORD_DTYPE) in file order.
         path: a verify path of the test hook after the count pass (0 =
         production split, 1 = header walk without the count pass's lists, 2 =
-        v3 with the lists); variant: an experiment arm of tools/experiments
+        v3 with the lists), or "one_pass" (the one-pass count + checksum
+        path, verify_fused.inc, then the production verify); variant: an experiment arm of tools/experiments
         (DESIGN.md 4.2)."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
@@ -199,7 +200,15 @@ class GpuContext:
         counts = self.alloc(4 * nblocks)
         first = self.alloc(4 * nblocks)
         L = lib()
-        check(L.revel_gpu_count_scan_records(self._h, image.ptr, nbytes, counts.ptr, first.ptr, None))
+        one_pass = path == "one_pass"
+        if one_pass:  # the one-pass count + checksum path (opt-in: REVEL_FUSED=1), then the production verify
+            path = None
+            prev = L.revel_debug_set_fused(1)
+        try:
+            check(L.revel_gpu_count_scan_records(self._h, image.ptr, nbytes, counts.ptr, first.ptr, None))
+        finally:
+            if one_pass:
+                L.revel_debug_set_fused(prev)
         tail_first = self.d2h(first, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         tail_count = self.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         total = int(tail_first) + int(tail_count)

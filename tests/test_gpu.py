@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from revel_amd import BLOCK_SIZE, env, log
-from revel_amd._lib import IO_ERROR, RevelError
+from revel_amd._lib import IO_ERROR, RevelError, check
 from revel_amd.gpu import RECORD_DTYPE
 from conftest import golden_image, trace
 from oracle import crc32c_oracle as po
@@ -146,14 +146,17 @@ def compare_walk(res, ref):
 
 
 # Verify paths: None = the C-ABI call sequence revel_gpu_count_scan_records
-# -> revel_gpu_verify_records (the count pass's own histogram + k_scan_order
-# build the block list; verify launches k_verify_rows + dense only); then the
-# test hook: 0 = the same density split with the block list built inside
-# verify (k_order_hist + k_order_scatter, as after the general scan), 1 = v3
-# walking the headers itself (verify without its count pass), 2 = v3 with the
-# header lists (unaligned images).  The experiment arms are checked in
-# test_experiments_gpu.py.
-VERIFY_PATHS = [None, 0, 1, 2]
+# -> revel_gpu_verify_records (the production default: k_count_hist +
+# k_scan_order, then k_verify_rows for blocks of up to 64 records and
+# k_verify_records_dense2 for the rest); "one_pass" = the same calls on the
+# opt-in one-pass path (REVEL_FUSED=1: k_walk_verify walks and checksums every
+# block in one read, verify expands its header lists, k_expand_fused, plus
+# k_verify_records_dense2 for the blocks it leaves); then the test hook after
+# the default count pass: 0 = the production verify, 1 = v3 walking the
+# headers itself (verify without its count pass), 2 = v3 with the count
+# pass's header lists (unaligned images), 3 = the round-4 split.
+# The experiment arms are checked in test_experiments_gpu.py.
+VERIFY_PATHS = [None, "one_pass", 0, 1, 2, 3]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)
@@ -1297,3 +1300,51 @@ def test_replay_sharded_verify_mode_and_context_lifetime(shard_ctxs):
     sh.close()
     with pytest.raises(RevelError):
         shard.ShardedReplay([shard_ctxs[0], shard_ctxs[0]], image=img)
+
+@pytest.mark.parametrize("tail", [1, 3, 7, 11])
+@pytest.mark.parametrize("slack", [0, 2, 6])
+def test_dense_block_then_tiny_tail(gpu_ctx, tail, slack):
+    """a dense block (> 64 records) whose last record ends 0-6 bytes
+    before the block end, followed by a final block of 1..11 bytes (a torn
+    header): the dense kernel's 16-B loads near that block's end may reach
+    past the image end, so they must be range-checked per dword; every verify
+    path equals the oracle walk, with a flipped bit in the dense block."""
+    rng = np.random.default_rng(1000 * tail + slack)
+    nrec = 150
+    body = 32768 - 7 * nrec - slack
+    cuts = np.sort(rng.choice(np.arange(1, body), nrec - 1, replace=False))
+    sizes = np.diff(np.concatenate([[0], cuts, [body]]))
+    recs = [rng.integers(0, 256, int(sz), dtype=np.uint8).tobytes() for sz in sizes]
+    img = bytearray(oc.write_image(recs))
+    img += bytes(slack)  # the writer leaves the last block's trailer out
+    assert len(img) == 32768
+    ref0 = oc.walk(bytes(img))
+    last = int(ref0["file_offset"][-1]) + 7
+    img[last + int(rng.integers(0, max(1, int(ref0["length"][-1]))))] ^= 0x40
+    img += bytes(rng.integers(0, 256, tail, dtype=np.uint8))
+    img = bytes(img)
+    ref = oc.walk(img)
+    assert int((ref["status"] == 1).sum()) == 1
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    for v in VERIFY_PATHS:
+        compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)
+
+
+def test_record_index_guard_rejects_u32_wrap(gpu_ctx):
+    """Record indices (d_first) are u32: the count calls and the shard loader
+    refuse an image whose physical records reach 2^32 (an image of empty
+    records past ~28 GiB) instead of wrapping -- the guard on a synthetic
+    counts array: 917 535 blocks x 4681 records = 4 294 981 335 > 2^32 - 1,
+    then 14 040 records fewer = exactly 2^32 - 1, which fits."""
+    from revel_amd._lib import lib
+    L = lib()
+    nb = 917535
+    counts = gpu_ctx.upload(np.full(nb, 4681, dtype=np.uint32))
+    with pytest.raises(RevelError, match="u32"):
+        check(L.revel_debug_check_record_index(gpu_ctx.handle, counts.ptr, nb))
+    gpu_ctx.h2d(counts, np.array([0, 0, 3], dtype=np.uint32))
+    check(L.revel_debug_check_record_index(gpu_ctx.handle, counts.ptr, nb))
+    # images that cannot wrap (at most 917 503 blocks) are not checked (no synchronisation)
+    gpu_ctx.h2d(counts, np.full(8, 0xFFFFFFFF, dtype=np.uint32))
+    check(L.revel_debug_check_record_index(gpu_ctx.handle, counts.ptr, 917503))
+    counts.free()

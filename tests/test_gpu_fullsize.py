@@ -267,3 +267,36 @@ def test_bench_c3_legs_report_both_timings(gpu_ctx, shape, monkeypatch):
     assert r["ms"] > 0 and r["ms_isolated"] > 0
     assert abs(r["value"] - r["per_rank_bytes"] / 2**30 / (r["ms"] / 1e3)) <= 0.05 * r["value"]
     assert "back to back" in r["timing"]
+
+
+def test_sharded_replay_one_context_per_device():
+    """One WAL across one context PER VISIBLE DEVICE (distinct GPUs; the
+    8-GPU node of the driver's round-end run): the stitched stream equals the
+    oracle Reader's.  Every other sharded test runs its contexts on device 0,
+    so this is the only test of distinct-device contexts; with one device
+    visible it skips."""
+    from revel_amd import gpu as G
+    ndev = G.device_count()
+    if ndev < 2:
+        pytest.skip(f"{ndev} gfx950 device visible: distinct-device contexts need 2 or more")
+    rng = np.random.default_rng(78)
+    sizes = rng.integers(0, 20000, 9000)
+    recs = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    img = oc.write_image(recs)
+    ctxs = [G.GpuContext(d) for d in range(ndev)]
+    try:
+        assert len({G.pci_bus_id(c.device) for c in ctxs}) == ndev
+        r = shard.ShardedReplay(ctxs, image=img, checksum=True, window_bytes=8 << 20)
+        got = []
+        while True:
+            x = r.read_record()
+            if x is None:
+                break
+            got.append(x)
+        assert got == recs
+        s = r.summary()
+        assert s["physical"] == len(oc.walk(img)) and s["bad"] == 0 and s["records"] == len(recs)
+        r.close()
+    finally:
+        for c in ctxs:
+            c.close()

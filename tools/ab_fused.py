@@ -1,0 +1,85 @@
+"""A/B of the C3 verify pipelines on one box, alternating: the one-pass
+count + checksum path (k_walk_verify -> scan -> k_expand_fused, round 5) vs
+the round-4 two-read path (k_count_hist -> k_scan_order -> k_verify_rows /
+k_verify_records_dense2), on bench.py's 4 GiB Zipf and small-record images.
+Checks both give identical results on every image.
+
+    python tools/ab_fused.py [--gib 4] [--rounds 4] [--iters 9]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=9)
+    ap.add_argument("--shapes", default="small,zipf")
+    a = ap.parse_args()
+    import bench
+    from revel_amd import gpu
+    from revel_amd._lib import lib
+    from revel_amd.gpu import RECORD_DTYPE
+    L = lib()
+    import ctypes
+    L.revel_debug_set_fused.restype = ctypes.c_int
+    L.revel_debug_set_fused.argtypes = [ctypes.c_int]
+    ctx = gpu.GpuContext(0)
+    out = {}
+    for shape in a.shapes.split(","):
+        seed = 0x5EED0003 if shape == "zipf" else 0x5EED0005
+        img, n, nrec = bench.c3_image(ctx, shape, seed, a.gib)
+        res = {}
+        digests = {}
+        for r in range(a.rounds):
+            for mode in (1, 0):
+                L.revel_debug_set_fused(mode)
+                streamed = []
+                times, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters, stream=streamed)
+                res.setdefault(mode, {"iso": [], "steady": []})
+                res[mode]["iso"].append(float(np.median(times)))
+                res[mode]["steady"].append(streamed[0])
+                if r == 0:
+                    # full result digest of the last call (every field)
+                    nblocks = (n + 32767) // 32768
+                    counts, first = ctx.alloc(4 * nblocks), ctx.alloc(4 * nblocks)
+                    o = ctx.alloc((nphys + 1) * RECORD_DTYPE.itemsize)
+                    from revel_amd._lib import check
+                    check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
+                    check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, o.ptr, None))
+                    ctx.sync()
+                    raw = ctx.d2h(o, nphys * RECORD_DTYPE.itemsize)
+                    import hashlib
+                    digests[mode] = (nphys, bad, hashlib.sha256(raw.tobytes()).hexdigest()[:16])
+                    for b in (counts, first, o):
+                        b.free()
+                print(json.dumps({"shape": shape, "round": r, "fused": mode, "ms_iso": round(res[mode]["iso"][-1], 4),
+                                  "ms_steady": round(res[mode]["steady"][-1], 4), "nphys": nphys, "bad": bad}),
+                      flush=True)
+        L.revel_debug_set_fused(-1)
+        img.free()
+        out[shape] = {
+            "bytes": n,
+            "fused_ms_steady_median": round(float(np.median(res[1]["steady"])), 4),
+            "legacy_ms_steady_median": round(float(np.median(res[0]["steady"])), 4),
+            "fused_ms_iso_median": round(float(np.median(res[1]["iso"])), 4),
+            "legacy_ms_iso_median": round(float(np.median(res[0]["iso"])), 4),
+            "identical_results": digests.get(1) == digests.get(0),
+            "digests": {str(k): v for k, v in digests.items()},
+        }
+        print(json.dumps({shape: out[shape]}), flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

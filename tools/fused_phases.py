@@ -1,0 +1,54 @@
+"""Phase breakdown of k_walk_verify (round 5): a build with
+-DREVEL_FUSED_PHASES sums each wave's shader-clock cycles per phase (loads
+landed, walk, chains + captures, scan, records) over the last count pass;
+this runs bench.py's image through the production count + verify and prints
+the per-block averages.
+
+    tools/build_variant.sh phases -DREVEL_FUSED_PHASES
+    python tools/fused_phases.py --lib build/ab/phases.so [--shape small]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("--shape", default="small")
+    ap.add_argument("--gib", type=float, default=4.0)
+    a = ap.parse_args()
+    from revel_amd import _lib
+    _lib.LIB_PATH = os.path.abspath(a.lib)
+    import bench
+    from revel_amd import gpu
+    ctx = gpu.GpuContext(0)
+    img, n, nrec = bench.c3_image(ctx, a.shape, 0x5EED0003 if a.shape == "zipf" else 0x5EED0005, a.gib)
+    L = _lib.lib()
+    f = L.revel_debug_fused_phases
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+    bench.c3_verify_timed(ctx, img, n, nrec, 1)  # warm
+    assert f(None, 1) == 0
+    t, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, 1)
+    buf = np.zeros(8, np.uint64)
+    assert f(buf.ctypes.data, 0) == 0
+    names = ["loads", "walk", "chains", "scan", "records"]
+    blocks, recs, waves = int(buf[5]), int(buf[6]), int(buf[7])
+    total = int(buf[:5].sum())
+    out = {"shape": a.shape, "ms": round(t[0], 4), "blocks": blocks, "records": recs, "waves": waves,
+           "cycles_per_block": {k: round(int(buf[i]) / max(1, blocks), 1) for i, k in enumerate(names)},
+           "share": {k: round(int(buf[i]) / max(1, total), 3) for i, k in enumerate(names)},
+           "wave_cycles_total_per_wave": round(total / max(1, waves)),
+           "walk_cycles_per_record": round(int(buf[1]) / max(1, recs), 1)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
