@@ -55,8 +55,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound on the CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
-    ap.add_argument("--e2e-gib", type=float, default=4.0,
-                    help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip)")
+    ap.add_argument("--e2e-gib", type=float, default=32.0,
+                    help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip; "
+                         "at most the --blocks image)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
     ap.add_argument("--c3-small-gib", type=float, default=4.0,
@@ -188,6 +189,27 @@ def pmc_traffic(nblocks: int):
                                            f"(sha256 {p['library_sha256'][:12]}), gfx950 FETCH_SIZE x2")
 
 
+def pmc_leg_traffic(leg: str, image_bytes: int):
+    """HBM bytes per call of a C3 leg (c3 / c3_small) from its committed
+    rocprofv3 PMC passes (profiles/pmc_<leg>.json, tools/pmc_summary.py
+    --pipeline): every dispatch of one count -> scan -> verify call, FETCH x2 +
+    WRITE -- only when those passes measured THIS librevel_wal.so on an image
+    of exactly these bytes.  Returns (bytes or None, source note)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{leg}.json")
+    try:
+        with open(path) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None, f"no PMC pass committed (profiles/pmc_{leg}.json)"
+    if p.get("library_sha256") != library_sha256():
+        return None, f"profiles/pmc_{leg}.json was taken on another build of librevel_wal.so"
+    if int(p.get("image_bytes") or -1) != image_bytes:
+        return None, f"profiles/pmc_{leg}.json was over a {p.get('image_bytes')} B image, not {image_bytes} B"
+    return p.get("hbm_bytes_per_call"), (f"profiles/pmc_{leg}.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                                          f"over {p.get('calls')} calls on this librevel_wal.so (sha256 "
+                                          f"{p['library_sha256'][:12]}), every dispatch of a call, FETCH x2")
+
+
 def cpu_baseline(ctx, dblocks, masked_dev, nblocks: int, seconds: float):
     """Oracle bytewise CRC (reference algorithm class) on one host core over a
     bounded sample of the same device blocks, repeated until ~`seconds` of CPU
@@ -306,11 +328,14 @@ def e2e_file_path(D) -> tuple:
     return d, os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{tag}.log")
 
 
+E2E_CHUNK = 1 << 30  # host bytes per piece of a rank's part (bounds the host copy at N ranks x 1 GiB)
+
+
 def e2e_write_file(D, per: int, part):
     """Write the shared WAL file for the end_to_end leg: rank 0 checks the
     free space for all ranks' parts (world x per bytes + 1 GiB) and creates
-    the file, then every rank writes its part (part() -> bytes of length per)
-    at rank x per.  A failure anywhere makes EVERY rank skip the leg together
+    the file, then every rank writes its part at rank x per, piece by piece
+    (part(offset, nbytes) -> bytes of that piece, E2E_CHUNK at a time).  A failure anywhere makes EVERY rank skip the leg together
     (the headline value is already measured and must still be printed).
     Returns (path, None), or (None, reason) after removing the file.
     REVEL_BENCH_E2E_FAIL_RANK=r makes rank r's write fail (CPU tests)."""
@@ -333,16 +358,17 @@ def e2e_write_file(D, per: int, part):
     try:
         if os.environ.get("REVEL_BENCH_E2E_FAIL_RANK") == str(D.rank):
             raise OSError(28, "injected write failure (REVEL_BENCH_E2E_FAIL_RANK)")
-        host = part()
         fd = os.open(path, os.O_WRONLY)
         try:
-            view = memoryview(host)
-            done = 0
-            while done < per:
-                done += os.pwrite(fd, view[done:], D.rank * per + done)
+            for off in range(0, per, E2E_CHUNK):
+                m = min(E2E_CHUNK, per - off)
+                view = memoryview(part(off, m))
+                done = 0
+                while done < m:
+                    done += os.pwrite(fd, view[done:], D.rank * per + off + done)
+                del view
         finally:
             os.close(fd)
-        del host, view
     except OSError as ex:
         ok, why = False, f"rank {D.rank} write: {ex}"
     if D.max(float(not ok)) > 0:
@@ -372,7 +398,7 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
     per = k * BLOCK_SIZE
     total = per * D.world
     # this rank's part of the WAL = its first k device blocks
-    path, why = e2e_write_file(D, per, lambda: ctx.d2h(dblocks, per))
+    path, why = e2e_write_file(D, per, lambda off, m: ctx.d2h(dblocks, m, src_offset=off))
     if path is None:
         return {"value": None, "skipped": why}
     D.barrier()
@@ -514,10 +540,25 @@ def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
     ms = streamed[0]
     ms_max = D.max(ms)
     iso_max = D.max(float(np.median(times)))
+    alg = n + 24 * nphys  # image read + 24-B result per physical record (rank 0's image)
+    traffic, traffic_source = pmc_leg_traffic("c3" if shape == "zipf" else "c3_small", n)
     return {
         "unit": "GiB/s",
         "value": round(n * D.world / 2**30 / (ms_max / 1e3), 1),
         "ms": round(ms_max, 4),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(alg / (ms / 1e3) / 1e9, 1),
+            "peak": PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(alg / (ms / 1e3) / 1e9 / PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_over_alg": round(traffic / alg, 3) if traffic else None,
+            "traffic_source": traffic_source,
+            "kernel_ms": round(ms, 4),
+            "kernel_ms_basis": "rank 0, steady state: the whole count -> scan -> verify call (all its launches)",
+            "alg_bytes_per_call": alg,
+        },
         "timing": f"{iters} calls queued back to back between one pair of HIP events (steady state, ms per call)",
         "ms_isolated": round(iso_max, 4),
         "value_isolated": round(n * D.world / 2**30 / (iso_max / 1e3), 1),
@@ -679,7 +720,7 @@ def dry_run(args, D):
     if args.e2e_gib > 0:
         k = min(args.blocks, int(args.e2e_gib * (1 << 30)) // BLOCK_SIZE)
         per = k * BLOCK_SIZE
-        path, why = e2e_write_file(D, per, lambda: np.zeros(per, np.uint8))
+        path, why = e2e_write_file(D, per, lambda off, m: np.zeros(m, np.uint8))
         size = os.path.getsize(path) if path else None
         D.barrier()
         if path and D.rank == 0:

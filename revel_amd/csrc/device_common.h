@@ -209,7 +209,12 @@ __device__ void fill_tables(uint32_t* tab) {
 // priorities a workgroup's older waves run ahead of its younger ones (the C2
 // kernel's waves finished at 2.6 / 3.5 / 4.4 / 4.9 ms of 5.2 by age rank,
 // profiles/r4/s20_*).  rotate_prio(r) sets priority r & 3; a wave calling it
-// with (its age rank + blocks done) takes every priority in turn.
+// with (its age rank + blocks done) takes every priority in turn.  A wave keeps
+// its last priority until it exits (a new wave starts at 0).  The gain was
+// measured with the verify kernels alone on their stream (DESIGN.md 4.2,
+// round 4); when other kernels share the CUs (C5 replay's copy-side count on
+// another stream, several contexts per device) the rotated waves issue ahead
+// of theirs part of the time -- not measured.
 __device__ __forceinline__ void rotate_prio(uint32_t r) {
     switch (__builtin_amdgcn_readfirstlane(r) & 3u) {
         case 0: __builtin_amdgcn_s_setprio(0); break;

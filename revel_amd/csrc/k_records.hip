@@ -1505,10 +1505,10 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
 // cycles per phase (reset = 1 zeroes them first, no copy)
 extern "C" int revel_debug_fused_phases(uint64_t* host, int reset) {
     if (reset) {
-        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        static const unsigned long long z[16] = {};
         return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fused_phase), z, sizeof z, 0, hipMemcpyHostToDevice);
     }
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_phase), 8 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_phase), 16 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
 }
 #endif
 #ifdef REVEL_ROWS_WAVETIME

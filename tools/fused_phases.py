@@ -34,19 +34,23 @@ def main():
     L = _lib.lib()
     f = L.revel_debug_fused_phases
     f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+    L.revel_debug_set_fused(1)  # the one-pass path (opt-in)
     bench.c3_verify_timed(ctx, img, n, nrec, 1)  # warm
     assert f(None, 1) == 0
     t, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, 1)
-    buf = np.zeros(8, np.uint64)
+    buf = np.zeros(16, np.uint64)
     assert f(buf.ctypes.data, 0) == 0
-    names = ["loads", "walk", "chains", "scan", "records"]
+    names = {0: "loads", 1: "walk_rest", 2: "chains", 3: "scan", 4: "records", 8: "detect", 9: "compact",
+             10: "successors", 11: "doubling", 12: "chain_end", 13: "scalar_walk"}
     blocks, recs, waves = int(buf[5]), int(buf[6]), int(buf[7])
-    total = int(buf[:5].sum())
+    total = int(sum(int(buf[i]) for i in names))
     out = {"shape": a.shape, "ms": round(t[0], 4), "blocks": blocks, "records": recs, "waves": waves,
-           "cycles_per_block": {k: round(int(buf[i]) / max(1, blocks), 1) for i, k in enumerate(names)},
-           "share": {k: round(int(buf[i]) / max(1, total), 3) for i, k in enumerate(names)},
+           "cycles_per_block": {k: round(int(buf[i]) / max(1, blocks), 1) for i, k in names.items()},
+           "share": {k: round(int(buf[i]) / max(1, total), 3) for i, k in names.items()},
            "wave_cycles_total_per_wave": round(total / max(1, waves)),
-           "walk_cycles_per_record": round(int(buf[1]) / max(1, recs), 1)}
+           "scalar_walks": {"continued": int(buf[14]), "from_start": int(buf[15]) & 0xFFFFFFFF,
+                            "overflow": int(buf[15]) >> 32},
+           "walk_cycles_per_record": round(sum(int(buf[i]) for i in (1, 8, 9, 10, 11, 12, 13)) / max(1, recs), 1)}
     print(json.dumps(out), flush=True)
 
 
