@@ -69,6 +69,13 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def progress(D, msg: str):
+    """A progress line on stderr (rank 0): long legs (the 32 GiB end-to-end
+    file) must not look hung to a supervisor watching the output."""
+    if D.rank == 0:
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def visible_gfx950() -> int:
     """gfx950 devices this process may use, counted WITHOUT initialising HIP
     (the launcher must not touch the GPU before it starts the ranks): KFD
@@ -633,19 +640,25 @@ def main(argv=None):
     achieved = alg_bytes / (kern_ms_max / 1e3) / 1e9
     traffic, traffic_source = pmc_traffic(n)
 
+    progress(D, f"C2 {kern_ms_max:.3f} ms per launch")
     e2e = None
     if args.e2e_gib > 0:
+        progress(D, f"end_to_end: writing and replaying a {args.e2e_gib:g} GiB-per-rank WAL file")
         e2e = end_to_end(ctx, D, dblocks, n, args.e2e_gib)
+        progress(D, f"end_to_end: {e2e.get('value')} GiB/s")
 
     c3 = None
     if args.c3_gib > 0:
         c3 = c3_records(ctx, D, args.c3_gib)
+        progress(D, f"c3: {c3['ms']} ms")
     c3_small = None
     if args.c3_small_gib > 0:
         c3_small = c3_records(ctx, D, args.c3_small_gib, shape="small")
+        progress(D, f"c3_small: {c3_small['ms']} ms")
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu:
+        progress(D, "cpu_baseline")
         cpu = cpu_baseline(ctx, dblocks, masked, n, args.cpu_seconds)
 
     if D.rank == 0:

@@ -948,6 +948,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 #include "verify_dense.inc"
 #include "verify_rows.inc"
 #include "verify_fused.inc"
+#include "verify_chunks.inc"
 
 // Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
@@ -1164,6 +1165,18 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
     return hipGetLastError();
 }
 
+// k_verify_dense_chunks for blocks of 65..256 records (round 5, measured
+// slower than dense2: opt-in with REVEL_DENSE_CHUNKS=1, or
+// revel_debug_set_dense_chunks for A/B tools).
+int g_dense_chunks_override = -1;
+bool dense_chunks_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("REVEL_DENSE_CHUNKS");
+        return v && v[0] == '1';
+    }();
+    return g_dense_chunks_override < 0 ? on : g_dense_chunks_override != 0;
+}
+
 // Verify (or FRAME: append framing) split by block density, from the
 // per-block record counts: the whole blocks with <= kListPerBlock records
 // through v3 (SPARSE_V5: the v5 experiment; verify only), every block with
@@ -1187,10 +1200,25 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
     const uint32_t grid =
         (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     if constexpr (!FRAME) {
-        if (lead == 0) {  // verify of a whole image: the aligned-word-stream kernel, every dense block
-            hipLaunchKernelGGL(k_verify_records_dense2<>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
-                               base_offset, d_first, d_out, hl, d_counts, dense_whole);
-            hipError_t e = hipGetLastError();
+        if (lead == 0) {  // verify of a whole image
+            hipError_t e = hipSuccess;
+            if (dense_chunks_enabled()) {
+                // blocks of 65..256 records: coalesced quarters + captures (verify_chunks.inc); then
+                // k_verify_records_dense2 over the rest -- more than 256 records, or marked
+                // capture-dense (records under ~60 B)
+                const uint32_t cgrid = (uint32_t)std::max<uint64_t>(
+                    1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + kChunkWaves - 1) / kChunkWaves));
+                hipLaunchKernelGGL(k_verify_dense_chunks, dim3(cgrid), dim3(kChunkThreads), 0, st, img, nbytes,
+                                   base_offset, d_first, d_out, const_cast<uint64_t*>(hl), d_counts, dense_whole);
+                e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL((k_verify_records_dense2<kListCap, true>), dim3(grid), dim3(kDenseThreads), 0, st,
+                                   img, nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole);
+            } else {  // the aligned-word-stream kernel over every dense block (round 4)
+                hipLaunchKernelGGL(k_verify_records_dense2<>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
+                                   base_offset, d_first, d_out, hl, d_counts, dense_whole);
+            }
+            e = hipGetLastError();
             if (e != hipSuccess || vbytes % kBlockSize == 0 || tail_in_rows) return e;
             hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0,
                                st, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, 0u);
@@ -1499,6 +1527,15 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
 }
 
 }  // namespace revel
+
+// A/B hook (not in the public header): 1 = k_verify_dense_chunks + dense2 over
+// the rest, 0 = dense2 over every dense block (round 4), -1 = REVEL_DENSE_CHUNKS's
+// choice.  Returns the previous setting.
+extern "C" int revel_debug_set_dense_chunks(int on) {
+    const int prev = revel::g_dense_chunks_override;
+    revel::g_dense_chunks_override = on < 0 ? -1 : (on ? 1 : 0);
+    return prev;
+}
 
 #ifdef REVEL_FUSED_PHASES
 // timing probe builds only (tools/fused_phases.py): k_walk_verify's summed

@@ -189,8 +189,10 @@ class GpuContext:
         WAL image.  Returns a structured array (RECORD_DTYPE) in file order.
         path: a verify path of the test hook after the count pass (0 =
         production split, 1 = header walk without the count pass's lists, 2 =
-        v3 with the lists), or "one_pass" (the one-pass count + checksum
-        path, verify_fused.inc, then the production verify); variant: an experiment arm of tools/experiments
+        v3 with the lists), "one_pass" (the one-pass count + checksum
+        path, verify_fused.inc, then the production verify) or "dense_chunks"
+        (the production verify with blocks of 65..256 records through the
+        opt-in k_verify_dense_chunks, verify_chunks.inc); variant: an experiment arm of tools/experiments
         (DESIGN.md 4.2)."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
@@ -217,6 +219,12 @@ class GpuContext:
             from ._lib import experiments  # kernel variants kept for the record (tools/experiments)
             check(experiments().revel_x_verify_records_variant(self._h, variant, image.ptr, nbytes, base_offset,
                                                                first.ptr, out.ptr, None))
+        elif path == "dense_chunks":  # blocks of 65..256 records through k_verify_dense_chunks (opt-in)
+            prev = L.revel_debug_set_dense_chunks(1)
+            try:
+                check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
+            finally:
+                L.revel_debug_set_dense_chunks(prev)
         elif path is not None:
             check(L.revel_gpu_verify_records_path(self._h, path, image.ptr, nbytes, base_offset, first.ptr, out.ptr,
                                                   None))

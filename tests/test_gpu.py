@@ -148,7 +148,9 @@ def compare_walk(res, ref):
 # Verify paths: None = the C-ABI call sequence revel_gpu_count_scan_records
 # -> revel_gpu_verify_records (the production default: k_count_hist +
 # k_scan_order, then k_verify_rows for blocks of up to 64 records and
-# k_verify_records_dense2 for the rest); "one_pass" = the same calls on the
+# k_verify_records_dense2 for the rest); "dense_chunks" = the same with the
+# opt-in k_verify_dense_chunks for blocks of 65..256 records (REVEL_DENSE_CHUNKS=1,
+# dense2 over the rest); "one_pass" = the same calls on the
 # opt-in one-pass path (REVEL_FUSED=1: k_walk_verify walks and checksums every
 # block in one read, verify expands its header lists, k_expand_fused, plus
 # k_verify_records_dense2 for the blocks it leaves); then the test hook after
@@ -156,7 +158,7 @@ def compare_walk(res, ref):
 # headers itself (verify without its count pass), 2 = v3 with the count
 # pass's header lists (unaligned images), 3 = the round-4 split.
 # The experiment arms are checked in test_experiments_gpu.py.
-VERIFY_PATHS = [None, "one_pass", 0, 1, 2, 3]
+VERIFY_PATHS = [None, "one_pass", "dense_chunks", 0, 1, 2, 3]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)
@@ -1348,3 +1350,69 @@ def test_record_index_guard_rejects_u32_wrap(gpu_ctx):
     gpu_ctx.h2d(counts, np.full(8, 0xFFFFFFFF, dtype=np.uint32))
     check(L.revel_debug_check_record_index(gpu_ctx.handle, counts.ptr, 917503))
     counts.free()
+
+
+def _block_of_records(rng, nrec, body):
+    """nrec records whose payloads fill `body` bytes (random cut points)."""
+    cuts = np.sort(rng.choice(np.arange(1, body), nrec - 1, replace=False))
+    sizes = np.diff(np.concatenate([[0], cuts, [body]]))
+    return [rng.integers(0, 256, int(sz), dtype=np.uint8).tobytes() for sz in sizes]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_dense_chunks_markers_and_reuse(gpu_ctx, seed):
+    """k_verify_dense_chunks (blocks of 65..256 records; the "dense_chunks" verify
+    path) against the oracle on
+    images that mix its blocks with the ones it hands to
+    k_verify_records_dense2: capture-dense blocks (a run of 20-40-B records,
+    more than three record starts in some 128-B chunk: marked in slot 256),
+    blocks past 256 records, sparse blocks, a zero record and a bad length
+    ending dense blocks, and bit flips everywhere.  Two different images
+    verified in turn on the SAME context (stale slot-256 values of the first
+    must not change the second's results), every verify path."""
+    rng = np.random.default_rng(4242 + seed)
+
+    def image(order):
+        recs = []
+        for kind in order:
+            if kind == "chunks":    # 120-220 records over a block: k_verify_dense_chunks
+                n = int(rng.integers(120, 220))
+                recs += _block_of_records(rng, n, 32768 - 7 * n)
+            elif kind == "capdense":  # 90 records, a run of 30 tiny ones inside
+                n = 90
+                tiny = [rng.integers(0, 256, int(rng.integers(20, 40)), dtype=np.uint8).tobytes() for _ in range(30)]
+                rest = _block_of_records(rng, n - 30, 32768 - 7 * n - sum(len(t) for t in tiny))
+                recs += rest[:20] + tiny + rest[20:]
+            elif kind == "over256":
+                n = 300
+                recs += _block_of_records(rng, n, 32768 - 7 * n)
+            else:  # sparse
+                n = 20
+                recs += _block_of_records(rng, n, 32768 - 7 * n)
+        img = bytearray(oc.write_image(recs))
+        ref = oc.walk(bytes(img))
+        for v in range(3, len(ref) - 1, 29):  # flips in every kind of block
+            off = int(ref["file_offset"][v]) + 7 + int(rng.integers(0, max(1, int(ref["length"][v]))))
+            img[off] ^= 1 << int(rng.integers(0, 8))
+        # a dense-chunks block ends early twice: a zero record, a length past the block end
+        for k, kind in enumerate(order):
+            if kind != "chunks":
+                continue
+            inb = np.flatnonzero(ref["file_offset"] // BLOCK_SIZE == k)
+            if len(inb) > 100:
+                z = int(ref["file_offset"][inb[int(rng.integers(70, 100))]])
+                if rng.integers(0, 2):
+                    img[z:z + 7] = b"\0" * 7
+                else:
+                    img[z + 4:z + 6] = (0xFFF0).to_bytes(2, "little")
+                break
+        return bytes(img)
+
+    kinds = ["chunks", "capdense", "chunks", "over256", "sparse", "chunks", "capdense", "chunks"]
+    imgs = [image(kinds), image(kinds[::-1])]
+    for img in imgs:
+        ref = oc.walk(img)
+        dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+        for v in VERIFY_PATHS:
+            compare_walk(gpu_ctx.verify_image(dimg, len(img), path=v), ref)
+        dimg.free()

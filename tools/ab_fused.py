@@ -1,10 +1,12 @@
-"""A/B of the C3 verify pipelines on one box, alternating: the one-pass
-count + checksum path (k_walk_verify -> scan -> k_expand_fused, round 5) vs
-the round-4 two-read path (k_count_hist -> k_scan_order -> k_verify_rows /
-k_verify_records_dense2), on bench.py's 4 GiB Zipf and small-record images.
-Checks both give identical results on every image.
+"""A/B of two C3 verify pipelines on one box, alternating, through a debug
+switch of the library (1 = arm A, 0 = arm B), on bench.py's 4 GiB Zipf and
+small-record images; checks both give identical results on every image.
+  --hook revel_debug_set_fused (default): the one-pass count + checksum path
+    (k_walk_verify -> scan -> k_expand_fused, round 5) vs the two-read path;
+  --hook revel_debug_set_dense_chunks: dense blocks by k_verify_dense_chunks
+    (+ dense2 over the rest, round 5) vs dense2 over all of them (round 4).
 
-    python tools/ab_fused.py [--gib 4] [--rounds 4] [--iters 9]
+    python tools/ab_fused.py [--hook NAME] [--gib 4] [--rounds 4] [--iters 9]
 """
 from __future__ import annotations
 
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--shapes", default="small,zipf")
+    ap.add_argument("--hook", default="revel_debug_set_fused")
     a = ap.parse_args()
     import bench
     from revel_amd import gpu
@@ -32,8 +35,9 @@ def main():
     from revel_amd.gpu import RECORD_DTYPE
     L = lib()
     import ctypes
-    L.revel_debug_set_fused.restype = ctypes.c_int
-    L.revel_debug_set_fused.argtypes = [ctypes.c_int]
+    hook = getattr(L, a.hook)
+    hook.restype = ctypes.c_int
+    hook.argtypes = [ctypes.c_int]
     ctx = gpu.GpuContext(0)
     out = {}
     for shape in a.shapes.split(","):
@@ -43,7 +47,7 @@ def main():
         digests = {}
         for r in range(a.rounds):
             for mode in (1, 0):
-                L.revel_debug_set_fused(mode)
+                hook(mode)
                 streamed = []
                 times, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters, stream=streamed)
                 res.setdefault(mode, {"iso": [], "steady": []})
@@ -63,17 +67,18 @@ def main():
                     digests[mode] = (nphys, bad, hashlib.sha256(raw.tobytes()).hexdigest()[:16])
                     for b in (counts, first, o):
                         b.free()
-                print(json.dumps({"shape": shape, "round": r, "fused": mode, "ms_iso": round(res[mode]["iso"][-1], 4),
+                print(json.dumps({"shape": shape, "round": r, "arm_on": mode, "ms_iso": round(res[mode]["iso"][-1], 4),
                                   "ms_steady": round(res[mode]["steady"][-1], 4), "nphys": nphys, "bad": bad}),
                       flush=True)
-        L.revel_debug_set_fused(-1)
+        hook(-1)
         img.free()
         out[shape] = {
             "bytes": n,
-            "fused_ms_steady_median": round(float(np.median(res[1]["steady"])), 4),
-            "legacy_ms_steady_median": round(float(np.median(res[0]["steady"])), 4),
-            "fused_ms_iso_median": round(float(np.median(res[1]["iso"])), 4),
-            "legacy_ms_iso_median": round(float(np.median(res[0]["iso"])), 4),
+            "hook": a.hook,
+            "on_ms_steady_median": round(float(np.median(res[1]["steady"])), 4),
+            "off_ms_steady_median": round(float(np.median(res[0]["steady"])), 4),
+            "on_ms_iso_median": round(float(np.median(res[1]["iso"])), 4),
+            "off_ms_iso_median": round(float(np.median(res[0]["iso"])), 4),
             "identical_results": digests.get(1) == digests.get(0),
             "digests": {str(k): v for k, v in digests.items()},
         }
