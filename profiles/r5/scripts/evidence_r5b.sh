@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 evidence on one box, every GPU step under its own time limit
+# Round-5 evidence, part B (part A: evidence_r5a.sh) on one box, every GPU step under its own time limit
 # (tools/box_step.sh stops the script on a fault-class exit status):
 #   1. the product GPU suite (-m gpu), smoke()
 #   2. bench.py (the driver's default command) and a rocprofv3 kernel trace of it
@@ -15,10 +15,6 @@ O=$R/gpurun_out/ev5_$tag
 mkdir -p "$O"
 export TMPDIR=/tmp
 step() { "$R/tools/box_step.sh" "$@" || exit 99; }
-step 600 "$O/pytest_product.log" python3 -u -m pytest "$R/tests" -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider
-step 120 "$O/smoke.log" python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()"
-step 420 "$O/bench.log" python3 "$R/bench.py"
-step 420 "$O/bench_trace.log" rocprofv3 --kernel-trace --stats -d "$O/bench_trace" -o bench -f csv -- python3 "$R/bench.py"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
