@@ -185,6 +185,7 @@ EXTRA_SIGNATURES = {
     "revel_debug_check_record_index": (c_int, [c_void_p, c_void_p, c_size_t]),
     "revel_debug_set_fused": (c_int, [c_int]),
     "revel_debug_set_dense_chunks": (c_int, [c_int]),
+    "revel_debug_set_dense_quad": (c_int, [c_int]),
 }
 
 # tools/experiments/libexperiments.so: kernel variants kept for the record

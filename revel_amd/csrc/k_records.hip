@@ -1177,6 +1177,19 @@ bool dense_chunks_enabled() {
     return g_dense_chunks_override < 0 ? on : g_dense_chunks_override != 0;
 }
 
+// k_verify_records_dense2 with quad-coalesced loads (round 5: bit-identical,
+// within noise of the lane-owned loads -- small records 2.242 vs 2.257 ms,
+// Zipf 0.766 vs 0.770, profiles/r5/r5h_ab_dense_quad.log -- so opt-in with
+// REVEL_DENSE_QUAD=1, or revel_debug_set_dense_quad for A/B tools).
+int g_dense_quad_override = -1;
+bool dense_quad_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("REVEL_DENSE_QUAD");
+        return v && v[0] == '1';
+    }();
+    return g_dense_quad_override < 0 ? on : g_dense_quad_override != 0;
+}
+
 // Verify (or FRAME: append framing) split by block density, from the
 // per-block record counts: the whole blocks with <= kListPerBlock records
 // through v3 (SPARSE_V5: the v5 experiment; verify only), every block with
@@ -1214,6 +1227,10 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
                 if (e != hipSuccess) return e;
                 hipLaunchKernelGGL((k_verify_records_dense2<kListCap, true>), dim3(grid), dim3(kDenseThreads), 0, st,
                                    img, nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole);
+            } else if (dense_quad_enabled()) {  // quad-coalesced loads (round 5)
+                hipLaunchKernelGGL((k_verify_records_dense2<kListPerBlock, false, true>), dim3(grid),
+                                   dim3(kDenseThreads), 0, st, img, nbytes, base_offset, d_first, d_out, hl, d_counts,
+                                   dense_whole);
             } else {  // the aligned-word-stream kernel over every dense block (round 4)
                 hipLaunchKernelGGL(k_verify_records_dense2<>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
                                    base_offset, d_first, d_out, hl, d_counts, dense_whole);
@@ -1534,6 +1551,14 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
 extern "C" int revel_debug_set_dense_chunks(int on) {
     const int prev = revel::g_dense_chunks_override;
     revel::g_dense_chunks_override = on < 0 ? -1 : (on ? 1 : 0);
+    return prev;
+}
+
+// A/B hook (not in the public header): 1 = dense2 with quad-coalesced loads,
+// 0 = lane-owned loads (round 4, the default), -1 = REVEL_DENSE_QUAD's choice.
+extern "C" int revel_debug_set_dense_quad(int on) {
+    const int prev = revel::g_dense_quad_override;
+    revel::g_dense_quad_override = on < 0 ? -1 : (on ? 1 : 0);
     return prev;
 }
 

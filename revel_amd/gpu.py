@@ -192,7 +192,8 @@ class GpuContext:
         v3 with the lists), "one_pass" (the one-pass count + checksum
         path, verify_fused.inc, then the production verify) or "dense_chunks"
         (the production verify with blocks of 65..256 records through the
-        opt-in k_verify_dense_chunks, verify_chunks.inc); variant: an experiment arm of tools/experiments
+        opt-in k_verify_dense_chunks, verify_chunks.inc) or "dense_quad"
+        (k_verify_records_dense2 with the opt-in quad-coalesced loads); variant: an experiment arm of tools/experiments
         (DESIGN.md 4.2)."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
@@ -225,6 +226,12 @@ class GpuContext:
                 check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
             finally:
                 L.revel_debug_set_dense_chunks(prev)
+        elif path == "dense_quad":  # dense2 with quad-coalesced loads (opt-in) instead of lane-owned ones
+            prev = L.revel_debug_set_dense_quad(1)
+            try:
+                check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
+            finally:
+                L.revel_debug_set_dense_quad(prev)
         elif path is not None:
             check(L.revel_gpu_verify_records_path(self._h, path, image.ptr, nbytes, base_offset, first.ptr, out.ptr,
                                                   None))

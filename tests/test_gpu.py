@@ -148,7 +148,8 @@ def compare_walk(res, ref):
 # Verify paths: None = the C-ABI call sequence revel_gpu_count_scan_records
 # -> revel_gpu_verify_records (the production default: k_count_hist +
 # k_scan_order, then k_verify_rows for blocks of up to 64 records and
-# k_verify_records_dense2 for the rest); "dense_chunks" = the same with the
+# k_verify_records_dense2 for the rest); "dense_quad" = the same with dense2's
+# opt-in quad-coalesced loads (REVEL_DENSE_QUAD=1); "dense_chunks" = the same with the
 # opt-in k_verify_dense_chunks for blocks of 65..256 records (REVEL_DENSE_CHUNKS=1,
 # dense2 over the rest); "one_pass" = the same calls on the
 # opt-in one-pass path (REVEL_FUSED=1: k_walk_verify walks and checksums every
@@ -158,7 +159,7 @@ def compare_walk(res, ref):
 # headers itself (verify without its count pass), 2 = v3 with the count
 # pass's header lists (unaligned images), 3 = the round-4 split.
 # The experiment arms are checked in test_experiments_gpu.py.
-VERIFY_PATHS = [None, "one_pass", "dense_chunks", 0, 1, 2, 3]
+VERIFY_PATHS = [None, "one_pass", "dense_chunks", "dense_quad", 0, 1, 2, 3]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)
