@@ -311,17 +311,18 @@ int ensure_fused_fb(revel_gpu_context* ctx) {
     return REVEL_OK;
 }
 
-// REVEL_FUSED=1 in the environment puts count_scan_records on the one-pass
-// count + checksum path (verify_fused.inc); the default is the two-read path
-// (count walk, then the verify kernels) until the one-pass kernel is faster
-// on every bench shape.  The A/B switch.
+// REVEL_FUSED=1 / 2 in the environment puts count_scan_records on a one-pass
+// count + checksum path (1: k_walk_verify, verify_fused.inc; 2: the streamed
+// k_walk_verify2, verify_fused2.inc); the default (0) is the two-read path
+// (count walk, then the verify kernels) until a one-pass kernel is faster on
+// every bench shape.  The A/B switch.
 int g_fused_override = -1;  // revel_debug_set_fused (A/B tools); -1 = the environment's choice
-bool fused_enabled() {
-    static const bool on = [] {
+int fused_mode() {
+    static const int env = [] {
         const char* v = getenv("REVEL_FUSED");
-        return v && v[0] == '1';
+        return v && (v[0] == '1' || v[0] == '2') ? v[0] - '0' : 0;
     }();
-    return g_fused_override < 0 ? on : g_fused_override != 0;
+    return g_fused_override < 0 ? env : g_fused_override;
 }
 
 // The u32 result index (d_first) of an image that could hold 2^32 or more
@@ -362,12 +363,12 @@ int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, si
     if (!d_image || !d_counts || !d_first) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     hipStream_t st = pick(ctx, stream);
-    if (fused_enabled() && revel::fused_capable(d_image)) {
+    if (fused_mode() && revel::fused_capable(d_image)) {
         // one read of the image: walk + every record's CRC (k_walk_verify), then the scan
         int rc = ensure_hlist(ctx, nblocks);
         if (!rc) rc = ensure_fused_fb(ctx);
         if (rc) return rc;
-        HIP_TRY(revel::fused_count(ctx->di, d_image, nbytes, d_counts, ctx->hlist, ctx->fused_fb, st),
+        HIP_TRY(revel::fused_count(ctx->di, d_image, nbytes, d_counts, ctx->hlist, ctx->fused_fb, st, fused_mode()),
                 "fused count launch");
         rc = revel_gpu_exclusive_scan_u32(ctx, d_counts, d_first, nblocks, st);
         if (rc) return rc;
@@ -567,11 +568,12 @@ int revel_debug_check_record_index(revel_gpu_context* ctx, const uint32_t* d_cou
     return check_record_index(ctx, d_counts, nblocks, ctx->stream);
 }
 
-// A/B hook (not in the public header): 1 = the one-pass count + checksum path,
-// 0 = the round-4 two-read path, -1 = REVEL_FUSED's choice.  Returns the previous setting.
+// A/B hook (not in the public header): 1 / 2 = a one-pass count + checksum
+// path (k_walk_verify / k_walk_verify2), 0 = the two-read path, -1 =
+// REVEL_FUSED's choice.  Returns the previous setting.
 int revel_debug_set_fused(int on) {
     const int prev = g_fused_override;
-    g_fused_override = on < 0 ? -1 : (on ? 1 : 0);
+    g_fused_override = on < 0 ? -1 : (on > 2 ? 1 : on);
     return prev;
 }
 

@@ -163,6 +163,7 @@ enum TableMode : int {
     TM_S4R = 0,  // slice-by-4, 32x replicated, 128 KiB LDS
     TM_S2R = 1,  // slice-by-2, 32x replicated, 64 KiB LDS
     TM_S4 = 2,   // slice-by-4, unreplicated, 4 KiB LDS (bank conflicts)
+    TM_S4H = 3,  // slice-by-4, 16x replicated, 64 KiB LDS (2-way conflicts, one stage per word; round 5)
 };
 
 template <int TM>
@@ -179,6 +180,10 @@ template <>
 struct TableCfg<TM_S4> {
     static constexpr uint32_t bytes = 4096;
 };
+template <>
+struct TableCfg<TM_S4H> {
+    static constexpr uint32_t bytes = 65536;
+};
 
 // Fill the LDS image of the tables (cooperatively, whole workgroup).
 template <int TM>
@@ -194,6 +199,10 @@ __device__ void fill_tables(uint32_t* tab) {
             uint32_t r = d >> 14, e = (d >> 6) & 255u, h = (d >> 5) & 1u;
             // byte0 -> T3 (r0 h0), byte1 -> T2 (r0 h1), byte2 -> T1 (r1 h0), byte3 -> T0 (r1 h1)
             v = c_tables.t[3 - (r * 2 + h)][e];
+        } else if constexpr (TM == TM_S4H) {
+            // row e (64 dw = 256 B) -> table slot k (16 dw) -> copy c (lane & 15): byte k of x -> T(3-k)
+            uint32_t e = d >> 6, k = (d >> 4) & 3u;
+            v = c_tables.t[3 - k][e];
         } else {
             // S2R: row e = [T1 x32 | T0 x32]
             uint32_t e = (d >> 6) & 255u, h = (d >> 5) & 1u;
@@ -232,6 +241,11 @@ __device__ __forceinline__ LaneConst make_lane_const() {
     uint32_t c4 = (lane_id() & 31u) << 2;
     return {c4, c4 | 0x10000u};
 }
+// TM_S4H: the lane's copy among 16
+__device__ __forceinline__ LaneConst make_lane_const_h() {
+    const uint32_t c4 = (lane_id() & 15u) << 2;
+    return {c4, c4};
+}
 
 // Absorb one little-endian 32-bit word into the raw register.
 template <int TM>
@@ -243,6 +257,14 @@ __device__ __forceinline__ uint32_t absorb(uint32_t crc, uint32_t w, LaneConst L
         uint32_t a2 = __builtin_amdgcn_perm(x, L.lc1, Sel<2>::v);
         uint32_t a3 = __builtin_amdgcn_perm(x, L.lc1, Sel<3>::v);
         return (ldsw<0>(tab, a0) ^ ldsw<128>(tab, a1)) ^ (ldsw<0>(tab, a2) ^ ldsw<128>(tab, a3));
+    } else if constexpr (TM == TM_S4H) {
+        // address = x_k << 8 | (lane & 15) << 2 (L.lc0 from make_lane_const_h), table k at +64 k
+        constexpr uint32_t s0 = 0x0C0C0400u, s1 = 0x0C0C0500u, s2 = 0x0C0C0600u, s3 = 0x0C0C0700u;
+        const uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, s0);
+        const uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, s1);
+        const uint32_t a2 = __builtin_amdgcn_perm(x, L.lc0, s2);
+        const uint32_t a3 = __builtin_amdgcn_perm(x, L.lc0, s3);
+        return (ldsw<0>(tab, a0) ^ ldsw<64>(tab, a1)) ^ (ldsw<128>(tab, a2) ^ ldsw<192>(tab, a3));
     } else if constexpr (TM == TM_S2R) {
         uint32_t a0 = __builtin_amdgcn_perm(x, L.lc0, Sel<0>::v);
         uint32_t a1 = __builtin_amdgcn_perm(x, L.lc0, Sel<1>::v);

@@ -110,7 +110,7 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
 // fused_verify expands the lists into d_out and checks those denser blocks.
 bool fused_capable(const void* d_image);
 hipError_t fused_count(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st);
+                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st, int variant = 1);
 hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
                         const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                         const uint32_t* d_counts, const uint32_t* d_fb, hipStream_t st);

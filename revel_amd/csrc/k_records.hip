@@ -949,6 +949,7 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 #include "verify_rows.inc"
 #include "verify_fused.inc"
 #include "verify_chunks.inc"
+#include "verify_fused2.inc"
 
 // Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
@@ -1374,13 +1375,20 @@ uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks) { return block_list
 bool fused_capable(const void* d_image) { return aligned16(d_image); }
 
 hipError_t fused_count(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st) {
+                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st, int variant) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (nblocks == 0) return hipSuccess;
     hipError_t e = ensure_len_tables(di, st);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(d_fb, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
+    if (variant == 2) {  // streamed (verify_fused2.inc): 12 waves per CU
+        const uint64_t grid2 = std::max<uint64_t>(
+            1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu), (nblocks + kF2Waves - 1) / kF2Waves));
+        hipLaunchKernelGGL(k_walk_verify2, dim3((uint32_t)grid2), dim3(kF2Threads), 0, st,
+                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_fb);
+        return hipGetLastError();
+    }
     // one workgroup per CU (the 128 KiB tables); waves loop over their blocks
     const uint64_t grid = std::max<uint64_t>(
         1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu), (nblocks + kFusedWaves - 1) / kFusedWaves));

@@ -203,10 +203,11 @@ class GpuContext:
         counts = self.alloc(4 * nblocks)
         first = self.alloc(4 * nblocks)
         L = lib()
-        one_pass = path == "one_pass"
-        if one_pass:  # the one-pass count + checksum path (opt-in: REVEL_FUSED=1), then the production verify
+        one_pass = path in ("one_pass", "one_pass2")
+        if one_pass:  # a one-pass count + checksum path (opt-in: REVEL_FUSED=1 / 2), then the production verify
+            mode = 2 if path == "one_pass2" else 1
             path = None
-            prev = L.revel_debug_set_fused(1)
+            prev = L.revel_debug_set_fused(mode)
         try:
             check(L.revel_gpu_count_scan_records(self._h, image.ptr, nbytes, counts.ptr, first.ptr, None))
         finally:

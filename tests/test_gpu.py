@@ -154,12 +154,13 @@ def compare_walk(res, ref):
 # dense2 over the rest); "one_pass" = the same calls on the
 # opt-in one-pass path (REVEL_FUSED=1: k_walk_verify walks and checksums every
 # block in one read, verify expands its header lists, k_expand_fused, plus
-# k_verify_records_dense2 for the blocks it leaves); then the test hook after
+# k_verify_records_dense2 for the blocks it leaves); "one_pass2" = the streamed
+# one-pass kernel (REVEL_FUSED=2, k_walk_verify2); then the test hook after
 # the default count pass: 0 = the production verify, 1 = v3 walking the
 # headers itself (verify without its count pass), 2 = v3 with the count
 # pass's header lists (unaligned images), 3 = the round-4 split.
 # The experiment arms are checked in test_experiments_gpu.py.
-VERIFY_PATHS = [None, "one_pass", "dense_chunks", "dense_quad", 0, 1, 2, 3]
+VERIFY_PATHS = [None, "one_pass", "one_pass2", "dense_chunks", "dense_quad", 0, 1, 2, 3]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--iters", type=int, default=9)
     ap.add_argument("--shapes", default="small,zipf")
     ap.add_argument("--hook", default="revel_debug_set_fused")
+    ap.add_argument("--on", type=int, default=1, help="the hook's value for arm A (arm B: 0)")
     a = ap.parse_args()
     import bench
     from revel_amd import gpu
@@ -46,8 +47,9 @@ def main():
         res = {}
         digests = {}
         for r in range(a.rounds):
-            for mode in (1, 0):
+            for mode in (a.on, 0):
                 hook(mode)
+                mode = 1 if mode else 0
                 streamed = []
                 times, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters, stream=streamed)
                 res.setdefault(mode, {"iso": [], "steady": []})

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--lib", required=True)
     ap.add_argument("--shape", default="small")
     ap.add_argument("--gib", type=float, default=4.0)
-    ap.add_argument("--kernel", choices=["fused", "chunks"], default="fused",
+    ap.add_argument("--kernel", choices=["fused", "fused2", "chunks"], default="fused",
                     help="fused: k_walk_verify (REVEL_FUSED=1); chunks: k_verify_dense_chunks (REVEL_DENSE_CHUNKS=1)")
     a = ap.parse_args()
     from revel_amd import _lib
@@ -36,7 +36,7 @@ def main():
     L = _lib.lib()
     f = L.revel_debug_fused_phases
     f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
-    L.revel_debug_set_fused(1 if a.kernel == "fused" else 0)  # the one-pass path (opt-in)
+    L.revel_debug_set_fused({"fused": 1, "fused2": 2}.get(a.kernel, 0))  # a one-pass path (opt-in)
     L.revel_debug_set_dense_chunks.restype, L.revel_debug_set_dense_chunks.argtypes = ctypes.c_int, [ctypes.c_int]
     L.revel_debug_set_dense_chunks(1 if a.kernel == "chunks" else -1)  # opt-in
     bench.c3_verify_timed(ctx, img, n, nrec, 1)  # warm
@@ -48,6 +48,8 @@ def main():
              10: "successors", 11: "doubling", 12: "chain_end", 13: "scalar_walk"}
     if a.kernel == "chunks":
         names = {0: "entries_issued", 1: "points_lookup", 2: "chains", 3: "scan", 4: "records"}
+    if a.kernel == "fused2":
+        names = {0: "stream", 1: "walk", 3: "scan", 4: "records"}
     blocks, recs, waves = int(buf[5]), int(buf[6]), int(buf[7])
     total = int(sum(int(buf[i]) for i in names))
     out = {"kernel": a.kernel, "shape": a.shape, "ms": round(t[0], 4), "blocks": blocks, "records": recs, "waves": waves,
@@ -55,7 +57,8 @@ def main():
            "share": {k: round(int(buf[i]) / max(1, total), 3) for i, k in names.items()},
            "wave_cycles_total_per_wave": round(total / max(1, waves)),
            "scalar_walks": {"continued": int(buf[14]), "from_start": int(buf[15]) & 0xFFFFFFFF,
-                            "overflow": int(buf[15]) >> 32} if a.kernel == "fused" else None,
+                            "overflow": int(buf[15]) >> 32} if a.kernel == "fused" else
+                           ({"scalar": int(buf[14]), "left_to_dense2": int(buf[15])} if a.kernel == "fused2" else None),
            "walk_cycles_per_record": round(sum(int(buf[i]) for i in (1, 8, 9, 10, 11, 12, 13)) / max(1, recs), 1)}
     print(json.dumps(out), flush=True)
 
