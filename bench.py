@@ -485,12 +485,12 @@ def c3_image(ctx, shape: str, seed: int, gib: float):
     return img, n, len(sizes)
 
 
-def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: None, stream=None):
+def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: None, stream=None, stream_runs: int = 1):
     """The production verify of a resident image through the C-ABI
     (revel_gpu_count_scan_records -> revel_gpu_verify_records), timed with
     HIP events around both calls, `iters` times, each call isolated (host
     sync after it).  With a list `stream`, then also `iters` calls queued back
-    to back, their ms per call appended to it.  Returns (per-iteration ms,
+    to back, `stream_runs` times, each run's ms per call appended to it.  Returns (per-iteration ms,
     physical records, records whose status is not OK: the last call's)."""
     from revel_amd._lib import check, lib
     from revel_amd.gpu import RECORD_DTYPE
@@ -513,16 +513,19 @@ def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: Non
     if stream is not None:
         # steady state: `iters` calls queued back to back (no host sync between
         # them, as a reader verifying window after window issues them), one
-        # pair of events around all: per call = elapsed / iters.  The isolated
-        # times above also hold the host's submission of the first launch after
-        # e0 (~20 us on an idle stream: `gap before` k_count_hist in the traces).
-        e0.record()
-        for _ in range(iters):
-            check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
-            check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, out.ptr, None))
-        e1.record()
-        ctx.sync()
-        stream.append(e0.elapsed_ms(e1) / iters)
+        # pair of events around all: per call = elapsed / iters, taken
+        # `stream_runs` times (a median and its spread, not one
+        # sample).  The isolated times above also hold the host's submission of
+        # the first launch after e0 (~20 us on an idle stream: `gap before`
+        # k_count_hist in the traces).
+        for _ in range(stream_runs):
+            e0.record()
+            for _ in range(iters):
+                check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
+                check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, out.ptr, None))
+            e1.record()
+            ctx.sync()
+            stream.append(e0.elapsed_ms(e1) / iters)
         barrier()
     nphys = int(ctx.d2h(first, 4 * nblocks, np.uint32)[-1]) + int(ctx.d2h(counts, 4 * nblocks, np.uint32)[-1])
     res = ctx.d2h(out, nphys * RECORD_DTYPE.itemsize).view(RECORD_DTYPE)
@@ -541,10 +544,10 @@ def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
     seed = (0x5EED0003 if shape == "zipf" else 0x5EED0005) ^ D.rank
     img, n, nrec = c3_image(ctx, shape, seed, gib)
     streamed = []
-    times, nphys, bad = c3_verify_timed(ctx, img, n, nrec, iters, D.barrier, stream=streamed)
+    times, nphys, bad = c3_verify_timed(ctx, img, n, nrec, iters, D.barrier, stream=streamed, stream_runs=3)
     img.free()
     bad = D.sum(float(bad))
-    ms = streamed[0]
+    ms = float(np.median(streamed))
     ms_max = D.max(ms)
     iso_max = D.max(float(np.median(times)))
     alg = n + 24 * nphys  # image read + 24-B result per physical record (rank 0's image)
@@ -566,7 +569,10 @@ def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
             "kernel_ms_basis": "rank 0, steady state: the whole count -> scan -> verify call (all its launches)",
             "alg_bytes_per_call": alg,
         },
-        "timing": f"{iters} calls queued back to back between one pair of HIP events (steady state, ms per call)",
+        "timing": f"median of {len(streamed)} runs of {iters} calls queued back to back between one pair of HIP "
+                  f"events (steady state, ms per call)",
+        "ms_runs_rank0": [round(x, 4) for x in streamed],
+        "spread_pct_rank0": round(100.0 * (max(streamed) - min(streamed)) / ms, 2),
         "ms_isolated": round(iso_max, 4),
         "value_isolated": round(n * D.world / 2**30 / (iso_max / 1e3), 1),
         "per_rank_bytes": n,

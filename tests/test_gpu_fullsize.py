@@ -267,6 +267,19 @@ def test_bench_c3_legs_report_both_timings(gpu_ctx, shape, monkeypatch):
     assert r["ms"] > 0 and r["ms_isolated"] > 0
     assert abs(r["value"] - r["per_rank_bytes"] / 2**30 / (r["ms"] / 1e3)) <= 0.05 * r["value"]
     assert "back to back" in r["timing"]
+    # the steady-state figure is the median of 3 runs, with their spread
+    runs = r["ms_runs_rank0"]
+    assert len(runs) == 3 and abs(r["ms"] - sorted(runs)[1]) <= 1e-3
+    assert r["spread_pct_rank0"] >= 0.0
+    # the leg's own roofline: image + 24 B per record over the steady-state time, against 8 TB/s
+    rf = r["roofline"]
+    alg = r["per_rank_bytes"] + 24 * r["physical_records_rank0"]
+    assert rf["alg_bytes_per_call"] == alg and rf["bound"] == "hbm" and rf["peak"] == bench.PEAK_GBS
+    # (kernel_ms is printed to 4 decimals: 0.1 % of a 64 MiB image's 0.05 ms)
+    assert abs(rf["achieved"] - alg / (rf["kernel_ms"] / 1e3) / 1e9) <= 0.005 * rf["achieved"]
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) <= 1e-3
+    # a 64 MiB image is not the committed PMC pass's: no traffic, and the reason says so
+    assert rf["traffic"] is None and ("image" in rf["traffic_source"] or "build" in rf["traffic_source"])
 
 
 def test_sharded_replay_one_context_per_device():
