@@ -1466,26 +1466,46 @@ hipError_t total_records(const DeviceInfo& di, const uint32_t* d_counts, uint64_
     return e;
 }
 
+// The workgroup size of k_count_hist / k_scan_order: 1024 (16 waves) puts
+// every chunk slot of an image up to 4096 chunks (128 Ki blocks) on its own
+// wave; 512 lets a wave walk two chunks in turn once the image passes 2048
+// chunks (bench.py's 4 GiB images have 2049).  Round 5, kernel traces over
+// four alternating processes (profiles/r5/late/count_wide_trace/): 930 vs
+// 950 us on small records, 58.3 vs 59.5 us on Zipf.  REVEL_COUNT_WIDE=0
+// restores 512 for A/B runs.
+static uint32_t count_threads() {
+    static const bool narrow = [] {
+        const char* v = getenv("REVEL_COUNT_WIDE");
+        return v && v[0] == '0';
+    }();
+    return narrow ? kCountThreads : kCountThreadsWide;
+}
+
 // The grid of k_count_hist and k_scan_order (they must agree: the same
 // workgroup visits the same chunks in both) and the chunk visiting mask.
-static void count_grid(const DeviceInfo& di, uint64_t nblocks, uint32_t* grid, uint32_t* cmask) {
+static void count_grid(const DeviceInfo& di, uint64_t nblocks, uint32_t threads, uint32_t* grid, uint32_t* cmask) {
     const uint64_t nchunks = (nblocks + 63) / 64;
+    const uint64_t waves = threads / 64;
     uint64_t p = 1;
     while (p < nchunks) p <<= 1;
     *cmask = (uint32_t)(p - 1);
     *grid = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>(std::min<uint64_t>(kOrderMaxWG, (uint64_t)std::max(1, di.num_cu)),
-                              (p + kCountWaves - 1) / kCountWaves));
+        1, std::min<uint64_t>(std::min<uint64_t>(kOrderMaxWG, (uint64_t)std::max(1, di.num_cu)), (p + waves - 1) / waves));
 }
 
 hipError_t count_hist(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                       uint64_t* d_hlist, uint32_t* d_wsums, uint32_t* d_aux, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (nblocks == 0) return hipSuccess;
+    const uint32_t threads = count_threads();
     uint32_t grid, cmask;
-    count_grid(di, nblocks, &grid, &cmask);
-    hipLaunchKernelGGL(k_count_hist, dim3(grid), dim3(kCountThreads), 0, st, static_cast<const uint8_t*>(d_image),
-                       nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
+    count_grid(di, nblocks, threads, &grid, &cmask);
+    if (threads == kCountThreadsWide)
+        hipLaunchKernelGGL(k_count_hist<kCountThreadsWide>, dim3(grid), dim3(threads), 0, st,
+                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
+    else
+        hipLaunchKernelGGL(k_count_hist<kCountThreads>, dim3(grid), dim3(threads), 0, st,
+                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
     return hipGetLastError();
 }
 
@@ -1493,10 +1513,15 @@ hipError_t scan_order(const DeviceInfo& di, uint64_t nbytes, const uint32_t* d_c
                       uint32_t* d_first, uint32_t* d_aux, hipStream_t st) {
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     if (nblocks == 0) return hipSuccess;
+    const uint32_t threads = count_threads();
     uint32_t grid, cmask;
-    count_grid(di, nblocks, &grid, &cmask);
-    hipLaunchKernelGGL(k_scan_order, dim3(grid), dim3(kCountThreads), 0, st, nbytes, d_counts, d_wsums, d_first, d_aux,
-                       cmask);
+    count_grid(di, nblocks, threads, &grid, &cmask);
+    if (threads == kCountThreadsWide)
+        hipLaunchKernelGGL(k_scan_order<kCountThreadsWide>, dim3(grid), dim3(threads), 0, st, nbytes, d_counts,
+                           d_wsums, d_first, d_aux, cmask);
+    else
+        hipLaunchKernelGGL(k_scan_order<kCountThreads>, dim3(grid), dim3(threads), 0, st, nbytes, d_counts, d_wsums,
+                           d_first, d_aux, cmask);
     return hipGetLastError();
 }
 
