@@ -221,9 +221,12 @@ __device__ void fill_tables(uint32_t* tab) {
 // with (its age rank + blocks done) takes every priority in turn.  A wave keeps
 // its last priority until it exits (a new wave starts at 0).  The gain was
 // measured with the verify kernels alone on their stream (DESIGN.md 4.2,
-// round 4); when other kernels share the CUs (C5 replay's copy-side count on
-// another stream, several contexts per device) the rotated waves issue ahead
-// of theirs part of the time -- not measured.
+// round 4).  With other work beside them (C5 replay: window i's verify while
+// window i+1 lands on the copy stream) the rotation measured neutral: 8 GiB
+// records-layout replay, rotation on / off (-DREVEL_DENSE_PRIO=0
+// -DREVEL_ROWS_PRIO=0), 6 alternating runs each: ring loader 50.1 / 50.4
+// GiB/s end to end, verify 585 / 580 GiB/s; whole-shard verify 5 652 / 5 458
+// GiB/s (profiles/r5/late/prio_e2e/).
 __device__ __forceinline__ void rotate_prio(uint32_t r) {
     switch (__builtin_amdgcn_readfirstlane(r) & 3u) {
         case 0: __builtin_amdgcn_s_setprio(0); break;
