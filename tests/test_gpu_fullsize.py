@@ -42,6 +42,16 @@ def test_c2_full_size_every_crc_vs_oracle(gpu_ctx):
             assert np.array_equal(want[:256], oc.full_block_crcs(host[:256], "bytewise"))
         # the stored header is what the writer would have stored
         assert np.array_equal(host[:, 0:4].copy().view(np.uint32).ravel(), want)
+    # the same 32 GiB through the C3 record path (count -> scan -> verify): 16 384
+    # 64-block chunks, so every count-pass wave walks several (kernel grid 4 096
+    # waves), the scan runs over 512 tiles, and the u32 record-index guard sums
+    # the counts (> 917 503 blocks); every block is one FULL record of 32 761 B
+    res = gpu_ctx.verify_image(d, n * BLOCK_SIZE)
+    assert len(res) == n
+    assert np.array_equal(res["file_offset"], np.arange(n, dtype=np.uint64) * BLOCK_SIZE)
+    assert (res["length"] == BLOCK_SIZE - 7).all() and (res["type"] == 1).all()
+    assert np.array_equal(res["stored_crc"], got) and np.array_equal(res["computed_crc"], got)
+    assert (res["status"] == 0).all()
     rng = np.random.default_rng(2)
     bad = np.sort(rng.choice(n, 257, replace=False))
     for b in bad:
@@ -51,6 +61,10 @@ def test_c2_full_size_every_crc_vs_oracle(gpu_ctx):
     gpu_ctx.crc_full_blocks(d, n, m, ok)
     gpu_ctx.sync()
     assert np.array_equal(np.flatnonzero(gpu_ctx.d2h(ok, n) == 0), bad)
+    res = gpu_ctx.verify_image(d, n * BLOCK_SIZE)
+    assert np.array_equal(np.flatnonzero(res["status"] != 0), bad)
+    assert (res["status"][bad] == 1).all()  # REVEL_REC_BAD_CHECKSUM
+    assert np.array_equal(res["stored_crc"], got)
 
 
 def test_c3_full_size_append_verify_roundtrip(gpu_ctx):

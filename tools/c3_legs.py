@@ -30,6 +30,7 @@ def main():
         print(json.dumps({"shape": shape, "ms_steady_median": round(float(np.median(streamed)), 4),
                           "ms_steady_runs": [round(x, 4) for x in streamed],
                           "ms_isolated_median": round(float(np.median(times)), 4), "nphys": nphys, "bad": bad,
+                          "image_bytes": n,
                           "env": {k: v for k, v in os.environ.items() if k.startswith("REVEL_")}}), flush=True)
 
 

@@ -44,10 +44,12 @@ def load_pipeline(d, first_kernel):
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv"))):
         with open(f) as fh:
             rows = list(csv.DictReader(fh))
-        start = min((int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == first_kernel), default=None)
+        # the first kernel by name prefix (k_count_hist is templated on its workgroup size)
+        first = [r for r in rows if short(r["Kernel_Name"]).startswith(first_kernel)]
+        start = min((int(r["Dispatch_Id"]) for r in first), default=None)
         if start is None:
             raise SystemExit(f"{f}: no {first_kernel} dispatch")
-        n = len({r["Dispatch_Id"] for r in rows if short(r["Kernel_Name"]) == first_kernel})
+        n = len({r["Dispatch_Id"] for r in first})
         if calls is not None and n != calls:
             raise SystemExit(f"{f}: {n} pipeline calls, other passes had {calls}")
         calls = n
