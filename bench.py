@@ -55,9 +55,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bound on the CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
-    ap.add_argument("--e2e-gib", type=float, default=32.0,
+    ap.add_argument("--e2e-gib", type=float, default=None,
                     help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip; "
-                         "at most the --blocks image)")
+                         "at most the --blocks image; default min(32, 100 / N): 32 GiB on one GPU, the "
+                         "100 GiB file of BASELINE config C5 from 4 GPUs on)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
     ap.add_argument("--c3-small-gib", type=float, default=4.0,
@@ -336,6 +337,15 @@ def e2e_file_path(D) -> tuple:
 
 
 E2E_CHUNK = 1 << 30  # host bytes per piece of a rank's part (bounds the host copy at N ranks x 1 GiB)
+
+
+def e2e_share(args, D) -> float:
+    """GiB of the shared WAL file per rank: --e2e-gib, or by default 32 GiB on
+    one GPU and min(32, 100 / N) on N, so the file (and the page cache it
+    fills) stays at C5's 100 GiB instead of growing to 32 N GiB."""
+    if args.e2e_gib is not None:
+        return args.e2e_gib
+    return min(32.0, 100.0 / D.world)
 
 
 def e2e_write_file(D, per: int, part):
@@ -648,9 +658,12 @@ def main(argv=None):
 
     progress(D, f"C2 {kern_ms_max:.3f} ms per launch")
     e2e = None
-    if args.e2e_gib > 0:
-        progress(D, f"end_to_end: writing and replaying a {args.e2e_gib:g} GiB-per-rank WAL file")
-        e2e = end_to_end(ctx, D, dblocks, n, args.e2e_gib)
+    e2e_gib = e2e_share(args, D)
+    if e2e_gib > 0:
+        progress(D, f"end_to_end: writing and replaying a {e2e_gib:g} GiB-per-rank WAL file")
+        e2e = end_to_end(ctx, D, dblocks, n, e2e_gib)
+        e2e["sizing"] = ("--e2e-gib" if args.e2e_gib is not None else
+                         "default: min(32, 100 / N) GiB per rank (BASELINE C5's 100 GiB file from 4 GPUs on)")
         progress(D, f"end_to_end: {e2e.get('value')} GiB/s")
 
     c3 = None
@@ -736,8 +749,9 @@ def dry_run(args, D):
     any failure) with zero bytes in place of the device blocks."""
     D.barrier()
     e2e = None
-    if args.e2e_gib > 0:
-        k = min(args.blocks, int(args.e2e_gib * (1 << 30)) // BLOCK_SIZE)
+    e2e_gib = e2e_share(args, D)
+    if e2e_gib > 0:
+        k = min(args.blocks, int(e2e_gib * (1 << 30)) // BLOCK_SIZE)
         per = k * BLOCK_SIZE
         path, why = e2e_write_file(D, per, lambda off, m: np.zeros(m, np.uint8))
         size = os.path.getsize(path) if path else None

@@ -156,3 +156,25 @@ def test_bench_gpus_8_e2e_skips_together(tmp_path):
     e = bad["end_to_end"]
     assert e["skipped"] and all(r["skipped"] for r in e["per_rank"])
     assert not os.listdir(tmp_path)
+
+
+def test_bench_e2e_share_default_keeps_c5_file_size():
+    """The end_to_end leg's default share: 32 GiB on one GPU,
+    min(32, 100 / N) on N ranks, so the shared file stays at BASELINE C5's
+    100 GiB instead of 32 N GiB; an explicit --e2e-gib wins."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class _D:
+        def __init__(self, world):
+            self.world = world
+
+    dflt = bench.parse([])
+    assert dflt.e2e_gib is None
+    assert bench.e2e_share(dflt, _D(1)) == 32.0
+    assert bench.e2e_share(dflt, _D(2)) == 32.0
+    assert bench.e2e_share(dflt, _D(4)) == 25.0
+    assert bench.e2e_share(dflt, _D(8)) == 12.5
+    assert bench.e2e_share(bench.parse(["--e2e-gib", "0"]), _D(8)) == 0.0
+    assert bench.e2e_share(bench.parse(["--e2e-gib", "3"]), _D(8)) == 3.0
