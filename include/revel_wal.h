@@ -248,10 +248,9 @@ int revel_gpu_frame_full_blocks(revel_gpu_context* ctx, void* d_blocks, size_t n
  * then overwrites with the results); without them verify walks the headers
  * itself, with the same results, slower.  A context's count -> verify pair
  * must not interleave with another on that context (use one context per
- * concurrent stream), and the image must not change between the two calls
- * (with REVEL_FUSED=1 in the environment, revel_gpu_count_scan_records checks
- * every record's CRC while it walks the headers -- one read of a 16-byte
- * aligned image -- and verify only writes the results).
+ * concurrent stream).  The verify pass reads the image itself: a change to
+ * the image between the two calls is seen by verify (its records' checksums),
+ * though the record layout comes from the count pass.
  * Record indices are u32: an image holding 2^32 or more physical records
  * (possible from ~28 GiB up: an empty record is 7 bytes, 4681 per block) is
  * refused by both count calls with REVEL_INVALID_ARGUMENT (the check sums the

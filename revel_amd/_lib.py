@@ -183,9 +183,6 @@ EXTRA_SIGNATURES = {
     "revel_gpu_verify_records_path": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p,
                                               c_void_p, c_void_p]),
     "revel_debug_check_record_index": (c_int, [c_void_p, c_void_p, c_size_t]),
-    "revel_debug_set_fused": (c_int, [c_int]),
-    "revel_debug_set_dense_chunks": (c_int, [c_int]),
-    "revel_debug_set_dense_quad": (c_int, [c_int]),
 }
 
 # tools/experiments/libexperiments.so: kernel variants kept for the record
@@ -199,6 +196,11 @@ EXPERIMENT_SIGNATURES = {
     "revel_x_walk_count_scan": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
     "revel_x_walk_verify": (c_int, [c_void_p, c_void_p, c_size_t, c_uint64, c_void_p, c_void_p, c_void_p,
                                     c_void_p]),
+    "revel_x_fused_count_scan": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+    "revel_x_fused_verify": (c_int, [c_void_p, c_void_p, c_size_t, c_uint64, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+    "revel_x_verify_dense_variant": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint64, c_void_p, c_void_p,
+                                             c_void_p]),
 }
 _xlib = None
 

@@ -56,7 +56,7 @@ void destroy_context(revel_gpu_context* ctx) {
     if (ctx->hlist) (void)hipFree(ctx->hlist);
     if (ctx->scan_scratch) (void)hipFree(ctx->scan_scratch);
     if (ctx->wsums) (void)hipFree(ctx->wsums);
-    if (ctx->fused_fb) (void)hipFree(ctx->fused_fb);
+    if (ctx->small_scratch) (void)hipFree(ctx->small_scratch);
     if (ctx->arena.base) (void)hipFree(ctx->arena.base);
     auto& pr = ctx->parked_reader;
     if (pr.h_win) (void)hipHostFree(pr.h_win);
@@ -301,45 +301,35 @@ int count_pass(revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint3
     ctx->hlist_nbytes = nbytes;
     ctx->hlist_counts = d_counts;
     ctx->hlist_list_ready = false;
-    ctx->hlist_fused = false;
     return REVEL_OK;
 }
 
-int ensure_fused_fb(revel_gpu_context* ctx) {
-    if (!ctx->fused_fb)  // [0] blocks past kListCap records, [2..3] a u64 of scratch
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->fused_fb), 4 * sizeof(uint32_t)), "hipMalloc(fused counters)");
+int ensure_small_scratch(revel_gpu_context* ctx) {
+    if (!ctx->small_scratch)
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->small_scratch), 4 * sizeof(uint32_t)), "hipMalloc(scratch)");
     return REVEL_OK;
-}
-
-// REVEL_FUSED=1 / 2 in the environment puts count_scan_records on a one-pass
-// count + checksum path (1: k_walk_verify, verify_fused.inc; 2: the streamed
-// k_walk_verify2, verify_fused2.inc); the default (0) is the two-read path
-// (count walk, then the verify kernels) until a one-pass kernel is faster on
-// every bench shape.  The A/B switch.
-int g_fused_override = -1;  // revel_debug_set_fused (A/B tools); -1 = the environment's choice
-int fused_mode() {
-    static const int env = [] {
-        const char* v = getenv("REVEL_FUSED");
-        return v && (v[0] == '1' || v[0] == '2') ? v[0] - '0' : 0;
-    }();
-    return g_fused_override < 0 ? env : g_fused_override;
 }
 
 // The u32 result index (d_first) of an image that could hold 2^32 or more
 // physical records: sum the counts in 64 bits and reject it (synchronises).
 int check_record_index(revel_gpu_context* ctx, const uint32_t* d_counts, uint64_t nblocks, hipStream_t st) {
     if (nblocks <= revel::kNoWrapBlocks) return REVEL_OK;
-    int rc = ensure_fused_fb(ctx);
+    int rc = ensure_small_scratch(ctx);
     if (rc) return rc;
     uint64_t total = 0;
-    HIP_TRY(revel::total_records(ctx->di, d_counts, nblocks, reinterpret_cast<unsigned long long*>(ctx->fused_fb + 2),
-                                 &total, st),
+    HIP_TRY(revel::total_records(ctx->di, d_counts, nblocks,
+                                 reinterpret_cast<unsigned long long*>(ctx->small_scratch + 2), &total, st),
             "total_records");
-    if (total > 0xFFFFFFFFull)
+    if (total > 0xFFFFFFFFull) {
+        // a verify of this image must not take the count pass's lists: its
+        // record slots (d_first) wrapped
+        ctx->hlist_image = nullptr;
+        ctx->hlist_list_ready = false;
         return set_error(REVEL_INVALID_ARGUMENT,
                          "image of %llu blocks holds %llu physical records: record indices (d_first) are u32, "
                          "verify at most 4294967295 records per call (split the image at a block boundary)",
                          (unsigned long long)nblocks, (unsigned long long)total);
+    }
     return REVEL_OK;
 }
 }  // namespace
@@ -363,22 +353,6 @@ int revel_gpu_count_scan_records(revel_gpu_context* ctx, const void* d_image, si
     if (!d_image || !d_counts || !d_first) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
     hipStream_t st = pick(ctx, stream);
-    if (fused_mode() && revel::fused_capable(d_image)) {
-        // one read of the image: walk + every record's CRC (k_walk_verify), then the scan
-        int rc = ensure_hlist(ctx, nblocks);
-        if (!rc) rc = ensure_fused_fb(ctx);
-        if (rc) return rc;
-        HIP_TRY(revel::fused_count(ctx->di, d_image, nbytes, d_counts, ctx->hlist, ctx->fused_fb, st, fused_mode()),
-                "fused count launch");
-        rc = revel_gpu_exclusive_scan_u32(ctx, d_counts, d_first, nblocks, st);
-        if (rc) return rc;
-        ctx->hlist_image = d_image;
-        ctx->hlist_nbytes = nbytes;
-        ctx->hlist_counts = d_counts;
-        ctx->hlist_list_ready = false;
-        ctx->hlist_fused = true;
-        return check_record_index(ctx, d_counts, nblocks, st);
-    }
     int rc = count_pass(ctx, d_image, nbytes, d_counts, st);
     if (rc) return rc;
     // one launch for the scan (first pass: the count pass's per-64-block sums)
@@ -413,13 +387,6 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     if (nbytes == 0) return REVEL_OK;
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
-    if (memo && ctx->hlist_fused) {
-        HIP_TRY(revel::fused_verify(ctx->di, d_image, nbytes, base_offset, d_first, d_out, ctx->hlist,
-                                    ctx->hlist_counts, ctx->fused_fb, pick(ctx, stream)),
-                "fused verify launch");
-        ctx->hlist_image = nullptr;
-        return REVEL_OK;
-    }
     HIP_TRY(revel::verify_records(ctx->di, d_image, nbytes, base_offset, d_first, d_out, memo ? ctx->hlist : nullptr,
                                   memo ? ctx->hlist_counts : nullptr, pick(ctx, stream),
                                   memo && ctx->hlist_list_ready),
@@ -428,11 +395,10 @@ int revel_gpu_verify_records(revel_gpu_context* ctx, const void* d_image, size_t
     return REVEL_OK;
 }
 
-// Test hook (not in the public header): the verify paths (0 = production --
-// the fused expand after a fused count pass, 1 = header walk without the
-// count pass's lists, 2 = v3 with the round-4 count pass's lists, 3 = the
-// round-4 split: k_verify_rows + k_verify_records_dense2).  Paths 2 and 3
-// after a fused count pass re-count the image with the round-4 count pass.
+// Test hook (not in the public header): the verify paths (0 = production,
+// 1 = header walk without the count pass's lists, 2 = v3 with the count
+// pass's lists, 3 = the round-4 split: k_verify_rows + k_verify_records_dense2,
+// which is the production split since round 4).
 int revel_gpu_verify_records_path(revel_gpu_context* ctx, int path, const void* d_image, size_t nbytes,
                                   uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                   void* stream) {
@@ -441,30 +407,9 @@ int revel_gpu_verify_records_path(revel_gpu_context* ctx, int path, const void* 
     if (!d_image || !d_first || !d_out) return set_error(REVEL_INVALID_ARGUMENT, "null device buffer");
     if (path < 0 || path > 3) return set_error(REVEL_INVALID_ARGUMENT, "verify path %d", path);
     const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
-    hipStream_t st = pick(ctx, stream);
-    if (path == 0 && memo && ctx->hlist_fused) {
-        ctx->hlist_image = nullptr;
-        HIP_TRY(revel::fused_verify(ctx->di, d_image, nbytes, base_offset, d_first, d_out, ctx->hlist,
-                                    ctx->hlist_counts, ctx->fused_fb, st),
-                "fused verify launch");
-        return REVEL_OK;
-    }
-    if (memo && ctx->hlist_fused && path >= 2) {
-        // the round-4 paths read the round-4 count pass's lists: re-count this image with it
-        // (same counts; d_first is the exclusive scan of those counts either way)
-        const uint64_t nblocks = (nbytes + REVEL_BLOCK_SIZE - 1) / REVEL_BLOCK_SIZE;
-        uint32_t* counts = const_cast<uint32_t*>(ctx->hlist_counts);
-        int rc = count_pass(ctx, d_image, nbytes, counts, st);
-        if (rc) return rc;
-        HIP_TRY(revel::scan_order(ctx->di, nbytes, counts, ctx->wsums, const_cast<uint32_t*>(d_first),
-                                  revel::block_list_of(ctx->hlist, nblocks), st),
-                "scan launch");
-        ctx->hlist_list_ready = true;
-    }
-    const bool memo2 = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
     HIP_TRY(revel::verify_records_path(ctx->di, path == 3 ? 0 : path, d_image, nbytes, base_offset, d_first, d_out,
-                                       memo2 ? ctx->hlist : nullptr, memo2 ? ctx->hlist_counts : nullptr, st,
-                                       memo2 && ctx->hlist_list_ready),
+                                       memo ? ctx->hlist : nullptr, memo ? ctx->hlist_counts : nullptr, pick(ctx, stream),
+                                       memo && ctx->hlist_list_ready),
             "verify_records_path launch");
     ctx->hlist_image = nullptr;
     return REVEL_OK;
@@ -566,15 +511,6 @@ int revel_gpu_event_free(revel_gpu_context* ctx, void* ev) {
 int revel_debug_check_record_index(revel_gpu_context* ctx, const uint32_t* d_counts, size_t nblocks) {
     CHECK_CTX(ctx);
     return check_record_index(ctx, d_counts, nblocks, ctx->stream);
-}
-
-// A/B hook (not in the public header): 1 / 2 = a one-pass count + checksum
-// path (k_walk_verify / k_walk_verify2), 0 = the two-read path, -1 =
-// REVEL_FUSED's choice.  Returns the previous setting.
-int revel_debug_set_fused(int on) {
-    const int prev = g_fused_override;
-    g_fused_override = on < 0 ? -1 : (on > 2 ? 1 : on);
-    return prev;
 }
 
 }  // extern "C"

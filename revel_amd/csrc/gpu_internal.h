@@ -102,18 +102,6 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
                           const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
                           const uint32_t* d_counts, hipStream_t st, bool list_ready = false);
 
-// The one-pass count + checksum path (verify_fused.inc): production for a
-// 16-B aligned image counted by revel_gpu_count_scan_records.  fused_count
-// walks every block, verifies the records of blocks with at most kListCap of
-// them and lists every block's headers in d_hlist (a mismatching record's
-// entry holds its computed CRC, bit 56 set); d_fb[0] = the blocks with more.
-// fused_verify expands the lists into d_out and checks those denser blocks.
-bool fused_capable(const void* d_image);
-hipError_t fused_count(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st, int variant = 1);
-hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                        const uint32_t* d_counts, const uint32_t* d_fb, hipStream_t st);
 // Physical records of an image whose u32 result index could wrap: a block
 // holds at most 32768 / 7 = 4681 records, so only images of more than
 // kNoWrapBlocks blocks (~28 GiB) can reach 2^32.  total_records sums the
@@ -264,8 +252,9 @@ struct revel_gpu_context {
     uint64_t hlist_nbytes = 0;
     const uint32_t* hlist_counts = nullptr;
     bool hlist_list_ready = false;  // the count pass also built verify's block list (count_scan_records)
-    bool hlist_fused = false;       // the count pass was fused_count: verify expands its lists (fused_verify)
-    uint32_t* fused_fb = nullptr;   // fused_count's counter of blocks past kListCap records (+ u64 scratch)
+    // 16 B of device scratch: the record-index guard's u64 sum (words 2..3);
+    // the experiment library (tools/experiments) also keeps a counter in word 0
+    uint32_t* small_scratch = nullptr;
     uint32_t* scan_scratch = nullptr;  // tile sums of revel_gpu_exclusive_scan_u32
     uint64_t scan_scratch_cap = 0;
     // per-64-block record sums of the last count pass (revel_gpu_count_records),

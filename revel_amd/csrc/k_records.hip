@@ -588,7 +588,7 @@ __global__ __launch_bounds__(THREADS) void k_verify_records2(const uint8_t* __re
 // 64 candidates' counts, then one set bit of the ballot per block.  Every
 // member is wave-uniform.
 // ---------------------------------------------------------------------------
-// MARK (one-pass path, verify_fused.inc): a block whose header list slot
+// MARK (the one-pass experiment, tools/experiments/x_verify_fused.inc): a block whose header list slot
 // kListCap holds kCapMarker qualifies too (walked and listed only, <= MINN records).
 constexpr uint64_t kCapMarker = ~0ull;
 template <bool DENSE, uint32_t MINN = kListPerBlock, bool MARK = false>
@@ -947,9 +947,6 @@ __global__ __launch_bounds__(kVerify2Threads) void k_verify_records3(const uint8
 
 #include "verify_dense.inc"
 #include "verify_rows.inc"
-#include "verify_fused.inc"
-#include "verify_chunks.inc"
-#include "verify_fused2.inc"
 
 // Header-list entries of records kListCap.. of the blocks that have more
 // (small-record logs: a 131-B record gives ~250 per block), one lane per block,
@@ -1166,38 +1163,6 @@ static hipError_t launch_verify3(uint64_t grid, bool partial, const uint8_t* img
     return hipGetLastError();
 }
 
-// k_verify_dense_chunks for blocks of 65..256 records (round 5, measured
-// slower than dense2: opt-in with REVEL_DENSE_CHUNKS=1, or
-// revel_debug_set_dense_chunks for A/B tools).
-int g_dense_chunks_override = -1;
-bool dense_chunks_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("REVEL_DENSE_CHUNKS");
-        return v && v[0] == '1';
-    }();
-    return g_dense_chunks_override < 0 ? on : g_dense_chunks_override != 0;
-}
-
-// k_verify_records_dense2 with quad-coalesced loads (round 5: bit-identical,
-// within noise of the lane-owned loads -- small records 2.242 vs 2.257 ms,
-// Zipf 0.766 vs 0.770, profiles/r5/r5h_ab_dense_quad.log -- so opt-in with
-// REVEL_DENSE_QUAD=1, or revel_debug_set_dense_quad for A/B tools).
-int g_dense_quad_override = -1;
-bool dense_quad_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("REVEL_DENSE_QUAD");
-        return v && v[0] == '1';
-    }();
-    return g_dense_quad_override < 0 ? on : g_dense_quad_override != 0;
-}
-
-// Verify (or FRAME: append framing) split by block density, from the
-// per-block record counts: the whole blocks with <= kListPerBlock records
-// through v3 (SPARSE_V5: the v5 experiment; verify only), every block with
-// more (partial first / last ones too) through k_verify_records_dense, and the
-// sparse partial blocks through the single-wave verify2 launch.  Each kernel
-// skips the others' blocks by count.  Lists: verify = hlist + overflow entries
-// in the result slots (xlist = out, 3 u64 apart); FRAME = framing list.
 // The blocks the sparse-block kernels leave: every block with more than
 // kListPerBlock records (partial first / last ones too) through
 // k_verify_records_dense, then the sparse partial blocks through the
@@ -1215,28 +1180,10 @@ static hipError_t launch_dense_and_partial(const DeviceInfo& di, const uint8_t* 
         (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + waves - 1) / waves));
     if constexpr (!FRAME) {
         if (lead == 0) {  // verify of a whole image
-            hipError_t e = hipSuccess;
-            if (dense_chunks_enabled()) {
-                // blocks of 65..256 records: coalesced quarters + captures (verify_chunks.inc); then
-                // k_verify_records_dense2 over the rest -- more than 256 records, or marked
-                // capture-dense (records under ~60 B)
-                const uint32_t cgrid = (uint32_t)std::max<uint64_t>(
-                    1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + kChunkWaves - 1) / kChunkWaves));
-                hipLaunchKernelGGL(k_verify_dense_chunks, dim3(cgrid), dim3(kChunkThreads), 0, st, img, nbytes,
-                                   base_offset, d_first, d_out, const_cast<uint64_t*>(hl), d_counts, dense_whole);
-                e = hipGetLastError();
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL((k_verify_records_dense2<kListCap, true>), dim3(grid), dim3(kDenseThreads), 0, st,
-                                   img, nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole);
-            } else if (dense_quad_enabled()) {  // quad-coalesced loads (round 5)
-                hipLaunchKernelGGL((k_verify_records_dense2<kListPerBlock, false, true>), dim3(grid),
-                                   dim3(kDenseThreads), 0, st, img, nbytes, base_offset, d_first, d_out, hl, d_counts,
-                                   dense_whole);
-            } else {  // the aligned-word-stream kernel over every dense block (round 4)
-                hipLaunchKernelGGL(k_verify_records_dense2<>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
-                                   base_offset, d_first, d_out, hl, d_counts, dense_whole);
-            }
-            e = hipGetLastError();
+            // the aligned-word-stream kernel over every dense block (round 4)
+            hipLaunchKernelGGL(k_verify_records_dense2<>, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
+                               base_offset, d_first, d_out, hl, d_counts, dense_whole);
+            hipError_t e = hipGetLastError();
             if (e != hipSuccess || vbytes % kBlockSize == 0 || tail_in_rows) return e;
             hipLaunchKernelGGL((k_verify_records2<FRAME, BP_BYTES, BS_PARTIAL, TM_S4, 64, true>), dim3(2), dim3(64), 0,
                                st, img, nbytes, base_offset, d_first, d_out, lead, hl, d_counts, xl, xs, 0u);
@@ -1371,75 +1318,6 @@ hipError_t verify_records(const DeviceInfo& di, const void* d_image, uint64_t nb
 
 uint32_t* block_list_of(uint64_t* d_hlist, uint64_t nblocks) { return block_list(d_hlist, nblocks); }
 
-// ---- the one-pass count + checksum path (verify_fused.inc) ----
-bool fused_capable(const void* d_image) { return aligned16(d_image); }
-
-hipError_t fused_count(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
-                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st, int variant) {
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    if (nblocks == 0) return hipSuccess;
-    hipError_t e = ensure_len_tables(di, st);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(d_fb, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    if (variant == 2) {  // streamed (verify_fused2.inc): 12 waves per CU
-        const uint64_t grid2 = std::max<uint64_t>(
-            1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu), (nblocks + kF2Waves - 1) / kF2Waves));
-        hipLaunchKernelGGL(k_walk_verify2, dim3((uint32_t)grid2), dim3(kF2Threads), 0, st,
-                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_fb);
-        return hipGetLastError();
-    }
-    // one workgroup per CU (the 128 KiB tables); waves loop over their blocks
-    const uint64_t grid = std::max<uint64_t>(
-        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu), (nblocks + kFusedWaves - 1) / kFusedWaves));
-    hipLaunchKernelGGL(k_walk_verify, dim3((uint32_t)grid), dim3(kFusedThreads), 0, st,
-                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_fb);
-    return hipGetLastError();
-}
-
-__global__ void k_list_overflow_gated(const uint8_t* __restrict__ image, uint64_t nbytes,
-                                      const uint32_t* __restrict__ counts, const uint32_t* __restrict__ first,
-                                      const uint64_t* __restrict__ hlist, revel_record_result* __restrict__ out,
-                                      const uint32_t* __restrict__ fb) {
-    if (__builtin_amdgcn_readfirstlane(*fb) == 0u) return;  // no block past kListCap records
-    const OverflowArgs ov{image, nbytes, first, hlist, out};
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
-         b += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t n = counts[b];
-        if (n > kListCap) list_overflow_block(ov, b, n);
-    }
-}
-
-hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
-                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
-                        const uint32_t* d_counts, const uint32_t* d_fb, hipStream_t st) {
-    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
-    if (nblocks == 0) return hipSuccess;
-    const uint8_t* img = static_cast<const uint8_t*>(d_image);
-    // blocks with more than kListCap records: their entries past 256 into their result slots,
-    // then k_verify_records_dense2 over exactly those blocks (both leave at once when fb[0] == 0)
-    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 4, (nblocks + 255) / 256));
-    hipLaunchKernelGGL(k_list_overflow_gated, dim3((uint32_t)g), dim3(256), 0, st, img, nbytes, d_counts, d_first,
-                       d_hlist, d_out, d_fb);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const uint64_t nchunks = (nblocks + kExpandBatch - 1) / kExpandBatch;
-    constexpr uint64_t kWaves = kExpandThreads / 64;
-    const uint64_t grid = std::max<uint64_t>(
-        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 8, (nchunks + kWaves - 1) / kWaves));
-    hipLaunchKernelGGL(k_expand_fused, dim3((uint32_t)grid), dim3(kExpandThreads), 0, st, img, nbytes, base_offset,
-                       d_first, d_out, d_hlist, d_counts);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const uint64_t dwaves = kDenseThreads / 64;
-    const uint32_t dgrid =
-        (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)di.num_cu, (nblocks + dwaves - 1) / dwaves));
-    hipLaunchKernelGGL((k_verify_records_dense2<kFusedCap, true>), dim3(dgrid), dim3(kDenseThreads), 0, st, img, nbytes,
-                       base_offset, d_first, d_out, d_hlist, d_counts, d_fb);
-    return hipGetLastError();
-}
-
 // Sum of the per-block counts in 64 bits (the u32 record-index guard).
 __global__ void k_sum_counts(const uint32_t* __restrict__ counts, uint64_t n, unsigned long long* __restrict__ total) {
     unsigned long long s = 0;
@@ -1468,18 +1346,11 @@ hipError_t total_records(const DeviceInfo& di, const uint32_t* d_counts, uint64_
 
 // The workgroup size of k_count_hist / k_scan_order: 1024 (16 waves) puts
 // every chunk slot of an image up to 4096 chunks (128 Ki blocks) on its own
-// wave; 512 lets a wave walk two chunks in turn once the image passes 2048
-// chunks (bench.py's 4 GiB images have 2049).  Round 5, kernel traces over
+// wave (512 lets a wave walk two chunks in turn once the image passes 2048
+// chunks; bench.py's 4 GiB images have 2049).  Round 5, kernel traces over
 // four alternating processes (profiles/r5/late/count_wide_trace/): 930 vs
-// 950 us on small records, 58.3 vs 59.5 us on Zipf.  REVEL_COUNT_WIDE=0
-// restores 512 for A/B runs.
-static uint32_t count_threads() {
-    static const bool narrow = [] {
-        const char* v = getenv("REVEL_COUNT_WIDE");
-        return v && v[0] == '0';
-    }();
-    return narrow ? kCountThreads : kCountThreadsWide;
-}
+// 950 us on small records, 58.3 vs 59.5 us on Zipf.
+static uint32_t count_threads() { return kCountThreadsWide; }
 
 // The grid of k_count_hist and k_scan_order (they must agree: the same
 // workgroup visits the same chunks in both) and the chunk visiting mask.
@@ -1500,12 +1371,8 @@ hipError_t count_hist(const DeviceInfo& di, const void* d_image, uint64_t nbytes
     const uint32_t threads = count_threads();
     uint32_t grid, cmask;
     count_grid(di, nblocks, threads, &grid, &cmask);
-    if (threads == kCountThreadsWide)
-        hipLaunchKernelGGL(k_count_hist<kCountThreadsWide>, dim3(grid), dim3(threads), 0, st,
-                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
-    else
-        hipLaunchKernelGGL(k_count_hist<kCountThreads>, dim3(grid), dim3(threads), 0, st,
-                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
+    hipLaunchKernelGGL(k_count_hist<kCountThreadsWide>, dim3(grid), dim3(threads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_wsums, d_aux, cmask);
     return hipGetLastError();
 }
 
@@ -1516,12 +1383,8 @@ hipError_t scan_order(const DeviceInfo& di, uint64_t nbytes, const uint32_t* d_c
     const uint32_t threads = count_threads();
     uint32_t grid, cmask;
     count_grid(di, nblocks, threads, &grid, &cmask);
-    if (threads == kCountThreadsWide)
-        hipLaunchKernelGGL(k_scan_order<kCountThreadsWide>, dim3(grid), dim3(threads), 0, st, nbytes, d_counts,
-                           d_wsums, d_first, d_aux, cmask);
-    else
-        hipLaunchKernelGGL(k_scan_order<kCountThreads>, dim3(grid), dim3(threads), 0, st, nbytes, d_counts, d_wsums,
-                           d_first, d_aux, cmask);
+    hipLaunchKernelGGL(k_scan_order<kCountThreadsWide>, dim3(grid), dim3(threads), 0, st, nbytes, d_counts, d_wsums,
+                       d_first, d_aux, cmask);
     return hipGetLastError();
 }
 
@@ -1578,34 +1441,6 @@ hipError_t frame_records(const DeviceInfo& di, const void* d_payloads, const Fra
 
 }  // namespace revel
 
-// A/B hook (not in the public header): 1 = k_verify_dense_chunks + dense2 over
-// the rest, 0 = dense2 over every dense block (round 4), -1 = REVEL_DENSE_CHUNKS's
-// choice.  Returns the previous setting.
-extern "C" int revel_debug_set_dense_chunks(int on) {
-    const int prev = revel::g_dense_chunks_override;
-    revel::g_dense_chunks_override = on < 0 ? -1 : (on ? 1 : 0);
-    return prev;
-}
-
-// A/B hook (not in the public header): 1 = dense2 with quad-coalesced loads,
-// 0 = lane-owned loads (round 4, the default), -1 = REVEL_DENSE_QUAD's choice.
-extern "C" int revel_debug_set_dense_quad(int on) {
-    const int prev = revel::g_dense_quad_override;
-    revel::g_dense_quad_override = on < 0 ? -1 : (on ? 1 : 0);
-    return prev;
-}
-
-#ifdef REVEL_FUSED_PHASES
-// timing probe builds only (tools/fused_phases.py): k_walk_verify's summed
-// cycles per phase (reset = 1 zeroes them first, no copy)
-extern "C" int revel_debug_fused_phases(uint64_t* host, int reset) {
-    if (reset) {
-        static const unsigned long long z[16] = {};
-        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fused_phase), z, sizeof z, 0, hipMemcpyHostToDevice);
-    }
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_phase), 16 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
-}
-#endif
 #ifdef REVEL_ROWS_WAVETIME
 // timing probe builds only (tools/rows_wavetime.py): k_verify_rows' per-wave
 // start / end times and block counts of its last launch

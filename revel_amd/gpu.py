@@ -189,11 +189,13 @@ class GpuContext:
         WAL image.  Returns a structured array (RECORD_DTYPE) in file order.
         path: a verify path of the test hook after the count pass (0 =
         production split, 1 = header walk without the count pass's lists, 2 =
-        v3 with the lists), "one_pass" (the one-pass count + checksum
-        path, verify_fused.inc, then the production verify) or "dense_chunks"
-        (the production verify with blocks of 65..256 records through the
-        opt-in k_verify_dense_chunks, verify_chunks.inc) or "dense_quad"
-        (k_verify_records_dense2 with the opt-in quad-coalesced loads); variant: an experiment arm of tools/experiments
+        v3 with the lists, 3 = the round-4 split); or one of round 5's
+        small-record kernels, kept in tools/experiments/libexperiments.so
+        (not the product): "one_pass" / "one_pass2"
+        (the one-pass count + checksum pair revel_x_fused_count_scan ->
+        revel_x_fused_verify), "dense_chunks" / "dense_quad" (the production
+        split with k_verify_dense_chunks or dense2's quad-coalesced loads for
+        the dense blocks); variant: an experiment arm of tools/experiments
         (DESIGN.md 4.2)."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
@@ -204,15 +206,12 @@ class GpuContext:
         first = self.alloc(4 * nblocks)
         L = lib()
         one_pass = path in ("one_pass", "one_pass2")
-        if one_pass:  # a one-pass count + checksum path (opt-in: REVEL_FUSED=1 / 2), then the production verify
-            mode = 2 if path == "one_pass2" else 1
-            path = None
-            prev = L.revel_debug_set_fused(mode)
-        try:
+        if one_pass:
+            from ._lib import experiments  # round 5's one-pass kernels (tools/experiments)
+            check(experiments().revel_x_fused_count_scan(self._h, 2 if path == "one_pass2" else 1, image.ptr, nbytes,
+                                                         counts.ptr, first.ptr, None))
+        else:
             check(L.revel_gpu_count_scan_records(self._h, image.ptr, nbytes, counts.ptr, first.ptr, None))
-        finally:
-            if one_pass:
-                L.revel_debug_set_fused(prev)
         tail_first = self.d2h(first, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         tail_count = self.d2h(counts, 4, np.uint32, src_offset=4 * (nblocks - 1))[0]
         total = int(tail_first) + int(tail_count)
@@ -221,18 +220,14 @@ class GpuContext:
             from ._lib import experiments  # kernel variants kept for the record (tools/experiments)
             check(experiments().revel_x_verify_records_variant(self._h, variant, image.ptr, nbytes, base_offset,
                                                                first.ptr, out.ptr, None))
-        elif path == "dense_chunks":  # blocks of 65..256 records through k_verify_dense_chunks (opt-in)
-            prev = L.revel_debug_set_dense_chunks(1)
-            try:
-                check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
-            finally:
-                L.revel_debug_set_dense_chunks(prev)
-        elif path == "dense_quad":  # dense2 with quad-coalesced loads (opt-in) instead of lane-owned ones
-            prev = L.revel_debug_set_dense_quad(1)
-            try:
-                check(L.revel_gpu_verify_records(self._h, image.ptr, nbytes, base_offset, first.ptr, out.ptr, None))
-            finally:
-                L.revel_debug_set_dense_quad(prev)
+        elif one_pass:
+            from ._lib import experiments
+            check(experiments().revel_x_fused_verify(self._h, image.ptr, nbytes, base_offset, counts.ptr, first.ptr,
+                                                     out.ptr, None))
+        elif path in ("dense_chunks", "dense_quad"):
+            from ._lib import experiments
+            check(experiments().revel_x_verify_dense_variant(self._h, 1 if path == "dense_chunks" else 2, image.ptr,
+                                                             nbytes, base_offset, first.ptr, out.ptr, None))
         elif path is not None:
             check(L.revel_gpu_verify_records_path(self._h, path, image.ptr, nbytes, base_offset, first.ptr, out.ptr,
                                                   None))

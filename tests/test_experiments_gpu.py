@@ -6,6 +6,7 @@ full parity suite in test_gpu.py."""
 import numpy as np
 import pytest
 
+import test_gpu
 from conftest import golden_image
 from oracle import oracle_c as oc
 from test_gpu import compare_walk, kat_blocks, run_full, zipf_image
@@ -80,3 +81,80 @@ def test_walk_pipeline_vs_oracle(gpu_ctx, golden_index):
     for img in images:
         dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
         compare_walk(walk_verify(gpu_ctx, dimg, len(img)), oc.walk(img))
+
+
+# ---- round 5's small-record kernels (moved out of the product in round 6) ----
+# "one_pass" / "one_pass2": the one-pass count + checksum pair
+# (revel_x_fused_count_scan mode 1 / 2 -> revel_x_fused_verify);
+# "dense_chunks" / "dense_quad": the production split with
+# k_verify_dense_chunks or dense2's quad-coalesced loads for the dense blocks
+# (revel_x_verify_dense_variant).  Every verify test of test_gpu.py that the
+# product runs over its VERIFY_PATHS runs here over these.
+EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad"]
+
+
+@pytest.fixture
+def experiment_paths(monkeypatch):
+    monkeypatch.setattr(test_gpu, "VERIFY_PATHS", EXPERIMENT_PATHS)
+
+
+@pytest.mark.parametrize("path", EXPERIMENT_PATHS)
+def test_exp_verify_golden_images(gpu_ctx, golden_index, path):
+    test_gpu.test_verify_golden_images(gpu_ctx, golden_index, path)
+
+
+@pytest.mark.parametrize("path", EXPERIMENT_PATHS)
+def test_exp_verify_zipf_and_corruption(gpu_ctx, path):
+    test_gpu.test_verify_zipf_and_corruption(gpu_ctx, path)
+
+
+@pytest.mark.parametrize("path", EXPERIMENT_PATHS)
+@pytest.mark.parametrize("cut", [1, 3, 6, 7, 8, 100, 32767, 32769, 40000])
+def test_exp_verify_partial_last_block(gpu_ctx, cut, path):
+    test_gpu.test_verify_partial_last_block(gpu_ctx, cut, path)
+
+
+def test_exp_loop_tests(gpu_ctx, experiment_paths):
+    """The product's loop-over-VERIFY_PATHS tests with the experiment paths."""
+    test_gpu.test_full_blocks_large_property(gpu_ctx)
+    test_gpu.test_expander_counts_1_to_64_with_flips(gpu_ctx)
+    for plen in [123, 124, 126, 127, 128, 251, 254, 255, 256]:
+        test_gpu.test_verify_dense_word_stream_edges(gpu_ctx, plen)
+    test_gpu.test_verify_small_records_dense(gpu_ctx)
+    for rec_len in [24, 100, 124, 200]:
+        test_gpu.test_verify_multi_batch_lists(gpu_ctx, rec_len)
+    test_gpu.test_verify_batch_start_on_16_byte_boundary(gpu_ctx)
+    for tail in ["dense", "sparse"]:
+        test_gpu.test_verify_mixed_density(gpu_ctx, tail)
+    test_gpu.test_property_dense_streams_vs_oracle(gpu_ctx)
+    for tail in [1, 3, 7, 11]:
+        for slack in [0, 2, 6]:
+            test_gpu.test_dense_block_then_tiny_tail(gpu_ctx, tail, slack)
+    for seed in [0, 1, 2]:
+        test_gpu.test_dense_chunks_markers_and_reuse(gpu_ctx, seed)
+
+
+@pytest.mark.parametrize("path", EXPERIMENT_PATHS + [None])
+@pytest.mark.parametrize("ending", ["zero", "bad_length"])
+def test_exp_256_records_then_bad_header(gpu_ctx, path, ending):
+    """a block of exactly 256 valid records followed by a
+    zero header or a length past the block end.  The one-pass kernels listed
+    such a block for dense2 with resume offset 0, so record 256 was re-read
+    from record 0's header; the oracle makes record 256 a status record."""
+    rng = np.random.default_rng(256)
+    n = 256
+    body = 32768 - 7 * n - 600  # room left for the bad header in the block
+    recs = test_gpu._block_of_records(rng, n, body)
+    img = bytearray(oc.write_image(recs))
+    off = len(img)  # header of record 256, inside block 0
+    assert off + 7 <= 32768
+    if ending == "zero":
+        img += bytes(7)
+    else:
+        img += bytes([1, 2, 3, 4]) + (0x7FF0).to_bytes(2, "little") + bytes([1])
+    img += bytes(32768 - len(img))  # pad the block
+    img = bytes(img)
+    ref = oc.walk(img)
+    assert len(ref) == n + 1 and ref["status"][n] != 0
+    dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
+    compare_walk(gpu_ctx.verify_image(dimg, len(img), path=path), ref)

@@ -148,19 +148,14 @@ def compare_walk(res, ref):
 # Verify paths: None = the C-ABI call sequence revel_gpu_count_scan_records
 # -> revel_gpu_verify_records (the production default: k_count_hist +
 # k_scan_order, then k_verify_rows for blocks of up to 64 records and
-# k_verify_records_dense2 for the rest); "dense_quad" = the same with dense2's
-# opt-in quad-coalesced loads (REVEL_DENSE_QUAD=1); "dense_chunks" = the same with the
-# opt-in k_verify_dense_chunks for blocks of 65..256 records (REVEL_DENSE_CHUNKS=1,
-# dense2 over the rest); "one_pass" = the same calls on the
-# opt-in one-pass path (REVEL_FUSED=1: k_walk_verify walks and checksums every
-# block in one read, verify expands its header lists, k_expand_fused, plus
-# k_verify_records_dense2 for the blocks it leaves); "one_pass2" = the streamed
-# one-pass kernel (REVEL_FUSED=2, k_walk_verify2); then the test hook after
-# the default count pass: 0 = the production verify, 1 = v3 walking the
-# headers itself (verify without its count pass), 2 = v3 with the count
-# pass's header lists (unaligned images), 3 = the round-4 split.
-# The experiment arms are checked in test_experiments_gpu.py.
-VERIFY_PATHS = [None, "one_pass", "one_pass2", "dense_chunks", "dense_quad", 0, 1, 2, 3]
+# k_verify_records_dense2 for the rest); then the test hook after the count
+# pass: 0 = the production verify, 1 = v3 walking the headers itself (verify
+# without its count pass), 2 = v3 with the count pass's header lists
+# (unaligned images), 3 = the round-4 split.  Round 5's small-record kernels
+# (one-pass, coalesced dense, quad loads) left the product in round 6: the
+# same tests run them over tools/experiments/libexperiments.so in
+# test_experiments_gpu.py (-m experiment).
+VERIFY_PATHS = [None, 0, 1, 2, 3]
 
 
 @pytest.mark.parametrize("path", VERIFY_PATHS)
@@ -1363,10 +1358,9 @@ def _block_of_records(rng, nrec, body):
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_dense_chunks_markers_and_reuse(gpu_ctx, seed):
-    """k_verify_dense_chunks (blocks of 65..256 records; the "dense_chunks" verify
-    path) against the oracle on
-    images that mix its blocks with the ones it hands to
-    k_verify_records_dense2: capture-dense blocks (a run of 20-40-B records,
+    """Dense-block shapes against the oracle (written for round 5's
+    k_verify_dense_chunks, now an experiment; its path re-runs this test in
+    test_experiments_gpu.py): images that mix 120-220-record blocks with capture-dense blocks (a run of 20-40-B records,
     more than three record starts in some 128-B chunk: marked in slot 256),
     blocks past 256 records, sparse blocks, a zero record and a bad length
     ending dense blocks, and bit flips everywhere.  Two different images

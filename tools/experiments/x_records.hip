@@ -5,8 +5,14 @@
 // to the production k_verify_rows: the round-1 kernel (v1), v2's boundary
 // paths, v3's load shapes (quad transpose, 64-B rounds), v5 and the register
 // ring.  Results: profiles/r1*_c3_*.txt, r2_c3_v7_vs_v3.txt; DESIGN.md section
-// 4.2.  Symbols are hidden except revel_x_verify_records_variant; the device
-// tables are this module's own copies (filled by its own k_init_len_tables).
+// 4.2.  Since round 6 it also holds round 5's small-record kernels, moved out
+// of the product: the one-pass count + checksum kernels
+// (x_verify_fused.inc, x_verify_fused2.inc), the coalesced dense kernel
+// (x_verify_chunks.inc) and dense2 with quad-coalesced loads
+// (x_verify_dense_quad.inc), each behind a revel_x_* entry point instead of
+// an environment switch.  Symbols are hidden except the revel_x_* functions;
+// the device tables are this module's own copies (filled by its own
+// k_init_len_tables).
 #include <vector>
 
 #include "k_records.hip"
@@ -16,6 +22,26 @@ namespace {
 #include "x_verify_ring.inc"
 #include "x_verify5.inc"
 #include "x_verify_walk.inc"
+#include "x_verify_fused.inc"
+#include "x_verify_chunks.inc"
+#include "x_verify_fused2.inc"
+#include "x_verify_dense_quad.inc"
+
+// Header-list entries past kListCap of the blocks the one-pass kernels left
+// (fb[0] counts them; none: the launch leaves at once).
+__global__ void k_list_overflow_gated(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                      const uint32_t* __restrict__ counts, const uint32_t* __restrict__ first,
+                                      const uint64_t* __restrict__ hlist, revel_record_result* __restrict__ out,
+                                      const uint32_t* __restrict__ fb) {
+    if (__builtin_amdgcn_readfirstlane(*fb) == 0u) return;
+    const OverflowArgs ov{image, nbytes, first, hlist, out};
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t n = counts[b];
+        if (n > kListCap) list_overflow_block(ov, b, n);
+    }
+}
 }  // namespace
 
 namespace revel {
@@ -384,8 +410,197 @@ hipError_t x_verify(const DeviceInfo& di, int variant, const void* d_image, uint
     }
 }
 
+// ---- round 5's one-pass count + checksum path (x_verify_fused.inc /
+// x_verify_fused2.inc), moved out of the product in round 6 ----
+hipError_t fused_count(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
+                       uint64_t* d_hlist, uint32_t* d_fb, hipStream_t st, int variant) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    hipError_t e = ensure_len_tables(di, st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(d_fb, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    if (variant == 2) {  // streamed: 12 waves per CU
+        hipLaunchKernelGGL(k_walk_verify2, dim3(grid_for(di, nblocks, kF2Waves)), dim3(kF2Threads), 0, st,
+                           static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_fb);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_walk_verify, dim3(grid_for(di, nblocks, kFusedWaves)), dim3(kFusedThreads), 0, st,
+                       static_cast<const uint8_t*>(d_image), nbytes, d_counts, d_hlist, d_fb);
+    return hipGetLastError();
+}
+
+hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint64_t base_offset,
+                        const uint32_t* d_first, revel_record_result* d_out, const uint64_t* d_hlist,
+                        const uint32_t* d_counts, const uint32_t* d_fb, hipStream_t st) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    if (nblocks == 0) return hipSuccess;
+    const uint8_t* img = static_cast<const uint8_t*>(d_image);
+    // blocks with more than kListCap records: their entries past 256 into their result slots,
+    // then k_verify_records_dense2 over exactly those blocks (both leave at once when fb[0] == 0)
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 4, (nblocks + 255) / 256));
+    hipLaunchKernelGGL(k_list_overflow_gated, dim3((uint32_t)g), dim3(256), 0, st, img, nbytes, d_counts, d_first,
+                       d_hlist, d_out, d_fb);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t nchunks = (nblocks + kExpandBatch - 1) / kExpandBatch;
+    constexpr uint64_t kWaves = kExpandThreads / 64;
+    const uint64_t grid = std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)std::max(1, di.num_cu) * 8, (nchunks + kWaves - 1) / kWaves));
+    hipLaunchKernelGGL(k_expand_fused, dim3((uint32_t)grid), dim3(kExpandThreads), 0, st, img, nbytes, base_offset,
+                       d_first, d_out, d_hlist, d_counts);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_verify_records_dense2<kFusedCap, true>), dim3(grid_for(di, nblocks, kDenseThreads / 64)),
+                       dim3(kDenseThreads), 0, st, img, nbytes, base_offset, d_first, d_out, d_hlist, d_counts, d_fb);
+    return hipGetLastError();
+}
+
+// The production split (k_verify_rows + expander over blocks of 1..64
+// records, after count_scan_records' block order) with another dense kernel:
+// dense = 1: k_verify_dense_chunks over blocks of 65..256 records, then
+// dense2 over the rest (more than 256, or marked capture-dense); dense = 2:
+// dense2 with quad-coalesced loads.  A 16-B aligned image only.
+hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* img, uint64_t nbytes,
+                                uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
+                                const uint64_t* hl, const uint32_t* d_counts, bool list_ready, hipStream_t st) {
+    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 2) return hipErrorInvalidValue;
+    hipError_t e = ensure_len_tables(di, st);
+    if (e != hipSuccess) return e;
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    uint32_t* d_blist = block_list(hl, nblocks);
+    const uint64_t* xl = reinterpret_cast<const uint64_t*>(d_out);
+    const uint32_t tail_bl = (uint32_t)(nbytes % kBlockSize);
+    uint64_t b_hi = nbytes / kBlockSize;
+    const bool tail_in_rows = tail_bl != 0;
+    const uint32_t tail_block = tail_in_rows ? (uint32_t)b_hi : 0xFFFFFFFFu;
+    if (tail_in_rows) ++b_hi;
+    const OverflowArgs ov{img, nbytes, d_first, hl, d_out};
+    if (!list_ready) {
+        e = launch_block_order(di, d_counts, 0u, (uint32_t)b_hi, d_blist, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_verify_rows<false, kRowsRing, kRowsThreads, 0>), dim3((uint32_t)std::max(1, di.num_cu)),
+                       dim3(kRowsThreads), 0, st, img, base_offset, d_first, d_out, 0u, hl, d_counts, xl,
+                       d_blist + kBlockListAux, d_blist, tail_block, tail_in_rows ? tail_bl : (uint32_t)kBlockSize, ov,
+                       kRowsDyn ? d_blist + 3 : nullptr);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = launch_expand_rows(di, base_offset, 0u, d_first, d_out, hl, d_counts, 0u, (uint32_t)b_hi, tail_block,
+                           tail_in_rows ? tail_bl : (uint32_t)kBlockSize, st);
+    if (e != hipSuccess) return e;
+    const uint32_t* dense_whole = d_blist + 1;
+    const uint32_t grid = grid_for(di, nblocks, kDenseThreads / 64);
+    if (dense == 1) {
+        hipLaunchKernelGGL(k_verify_dense_chunks, dim3(grid_for(di, nblocks, kChunkWaves)), dim3(kChunkThreads), 0, st,
+                           img, nbytes, base_offset, d_first, d_out, const_cast<uint64_t*>(hl), d_counts, dense_whole);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_verify_records_dense2<kListCap, true>), dim3(grid), dim3(kDenseThreads), 0, st, img,
+                           nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole);
+    } else {
+        hipLaunchKernelGGL((k_verify_records_dense2q<>), dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
+                           base_offset, d_first, d_out, hl, d_counts, dense_whole);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
 }  // namespace revel
+
+namespace {
+hipStream_t x_stream(revel_gpu_context* ctx, void* stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+int x_hlist(revel_gpu_context* ctx, uint64_t nblocks) {
+    if (nblocks > ctx->hlist_cap_blocks) {
+        if (ctx->hlist) (void)hipFree(ctx->hlist);
+        ctx->hlist = nullptr;
+        ctx->hlist_cap_blocks = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->hlist), revel::hlist_words(nblocks) * sizeof(uint64_t)) !=
+            hipSuccess)
+            return REVEL_IO_ERROR;
+        ctx->hlist_cap_blocks = nblocks;
+    }
+    if (!ctx->small_scratch &&
+        hipMalloc(reinterpret_cast<void**>(&ctx->small_scratch), 4 * sizeof(uint32_t)) != hipSuccess)
+        return REVEL_IO_ERROR;
+    return REVEL_OK;
+}
+}  // namespace
+
+// Round 5's one-pass path (mode 1: k_walk_verify; 2: the streamed
+// k_walk_verify2) on a product context, as the pair revel_x_fused_count_scan
+// -> revel_x_fused_verify: the first call walks every block and checksums the
+// records of blocks with at most 256 of them in one read of the image, the
+// second expands the header lists into d_out and checks the blocks it left
+// (the image must not change between them).  16-B aligned images only
+// (REVEL_NOT_SUPPORT otherwise).  The product's verify cannot take these
+// lists (its memo is cleared).
+extern "C" __attribute__((visibility("default"))) int revel_x_fused_count_scan(
+    revel_gpu_context* ctx, int mode, const void* d_image, size_t nbytes, uint32_t* d_counts, uint32_t* d_first,
+    void* stream) {
+    if (!ctx || !d_image || !d_counts || !d_first || mode < 1 || mode > 2) return REVEL_INVALID_ARGUMENT;
+    if (nbytes == 0) return REVEL_OK;
+    if ((reinterpret_cast<uintptr_t>(d_image) & 15u) != 0) return REVEL_NOT_SUPPORT;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    int rc = x_hlist(ctx, nblocks);
+    if (rc) return rc;
+    hipStream_t st = x_stream(ctx, stream);
+    hipError_t e = revel::fused_count(ctx->di, d_image, nbytes, d_counts, ctx->hlist, ctx->small_scratch, st, mode);
+    if (e == hipSuccess) e = revel::exclusive_scan_t<uint32_t>(d_counts, d_first, nblocks,
+                                                                 reinterpret_cast<uint32_t*>(ctx->hlist) +
+                                                                     2 * nblocks * kListStride,
+                                                                 st);
+    ctx->hlist_image = nullptr;
+    return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
+extern "C" __attribute__((visibility("default"))) int revel_x_fused_verify(
+    revel_gpu_context* ctx, const void* d_image, size_t nbytes, uint64_t base_offset, const uint32_t* d_counts,
+    const uint32_t* d_first, revel_record_result* d_out, void* stream) {
+    if (!ctx || !d_image || !d_counts || !d_first || !d_out) return REVEL_INVALID_ARGUMENT;
+    if (nbytes == 0) return REVEL_OK;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    hipError_t e = revel::fused_verify(ctx->di, d_image, nbytes, base_offset, d_first, d_out, ctx->hlist, d_counts,
+                                       ctx->small_scratch, x_stream(ctx, stream));
+    return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
+
+// The production split with another dense kernel (1: k_verify_dense_chunks +
+// dense2 over the rest; 2: dense2 with quad-coalesced loads), after
+// revel_gpu_count_scan_records of the same image on this context (its header
+// lists and block order).
+extern "C" __attribute__((visibility("default"))) int revel_x_verify_dense_variant(
+    revel_gpu_context* ctx, int dense, const void* d_image, size_t nbytes, uint64_t base_offset,
+    const uint32_t* d_first, revel_record_result* d_out, void* stream) {
+    if (!ctx || !d_image || !d_first || !d_out) return REVEL_INVALID_ARGUMENT;
+    if (nbytes == 0) return REVEL_OK;
+    revel::DeviceGuard guard(ctx->di.device);
+    if (guard.err() != hipSuccess) return REVEL_IO_ERROR;
+    const bool memo = ctx->hlist && ctx->hlist_image == d_image && ctx->hlist_nbytes == nbytes;
+    if (!memo) return REVEL_INVALID_ARGUMENT;
+    hipError_t e = revel::verify_dense_variant(ctx->di, dense, static_cast<const uint8_t*>(d_image), nbytes,
+                                               base_offset, d_first, d_out, ctx->hlist, ctx->hlist_counts,
+                                               ctx->hlist_list_ready, x_stream(ctx, stream));
+    ctx->hlist_image = nullptr;
+    if (e == hipErrorInvalidValue) return REVEL_INVALID_ARGUMENT;
+    return e == hipSuccess ? REVEL_OK : REVEL_IO_ERROR;
+}
+
+#ifdef REVEL_FUSED_PHASES
+// timing probe builds only (tools/fused_phases.py): k_walk_verify's summed
+// cycles per phase (reset = 1 zeroes them first, no copy)
+extern "C" __attribute__((visibility("default"))) int revel_x_fused_phases(uint64_t* host, int reset) {
+    if (reset) {
+        static const unsigned long long z[16] = {};
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fused_phase), z, sizeof z, 0, hipMemcpyHostToDevice);
+    }
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_phase), 16 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // Verify variant `variant` (numbering of DESIGN.md section 4.2) on a product
 // context; uses the header lists of the context's last count pass when they
