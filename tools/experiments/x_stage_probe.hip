@@ -1,0 +1,258 @@
+// x_stage_probe.hip -- probe (round 6, VERDICT r5 #1 go / no-go): the
+// small-record verify as ONE coalesced read per block, staged in LDS.
+//
+// One workgroup of 4 waves per CU; each wave owns a 32 KiB LDS slot; the
+// slice-by-4 tables take the other 32 KiB (160 KiB in all).  Per block a wave
+//   1. LOADS the block into its slot: 32 global_load_lds_dwordx4 (1 KiB rows,
+//      C2's coalesced pattern), then vmcnt(0);
+//   2. WALKS the headers from LDS (log_reader.rs:155-216 / the oracle's walk:
+//      a trailer < 7 B ends the block, a zero record or a length past the end
+//      ends it with a status record), every lane computing the same wave-
+//      uniform hop, record k's offset into lane k & 63 of offs[k >> 6];
+//   3. CHECKSUMS the records lane-per-record from LDS (CH records per lane in
+//      flight), each as an aligned word stream (dense2's: word k =
+//      alignbyte(raw k + 1, raw k, s & 3), the last word masked, x^(-8 pad)
+//      at the end), crc = mask(raw ^ init_xor(len + 1)) as log_writer.rs:107-111.
+// Tables: 8 replicas of T0..T3, word e * 32 + m * 8 + r holds T_m[e].  Lane l
+// uses replica r = l & 7 and takes the four bytes of x in the order rotated
+// by q = (l >> 3) & 3, so in each ds_read_b32 the 32 lanes of a half-wave
+// hit 32 distinct banks (m * 8 + r): conflict-free with 32 KiB, at the price
+// of a shift after the v_perm that builds the address.
+// Output: counts[b], the computed masked CRC of record k < 256 of block b at
+// crcs[256 b + k], and per-phase shader cycles summed over waves in stats
+// ([0] load, [1] walk, [2] checksums, [3] blocks, [4] records whose computed
+// CRC differs from the stored one, [5] records).  Timing probe + parity check
+// only; built into tools/experiments/libxst.so (make -C tools/experiments xst).
+#include "device_common.h"
+
+namespace {
+
+constexpr int kStThreads = 256;            // 4 waves: one slot each
+constexpr uint32_t kSlotDw = kBlockSize / 4;  // 8192 dwords
+constexpr uint32_t kTabDw = 8192;          // 32 KiB of tables
+
+__device__ uint32_t g_st_init_xor[kBlockSize + 2];
+__device__ uint32_t g_st_x8inv[4];  // x^(-8 pad), pad = 0..3
+
+__global__ void k_st_init() {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d <= kBlockSize + 1u; d += gridDim.x * blockDim.x) {
+        uint32_t x = 0x80000000u, a = x8n(1), n = d;
+        while (n) {
+            if (n & 1u) x = multmodp(x, a);
+            a = multmodp(a, a);
+            n >>= 1;
+        }
+        g_st_init_xor[d] = multmodp(x, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 4) {
+        // x^-8 = x^(2^32 - 1 - 8) mod P is awkward; use x^-1 = (P + 1) / x (reflected 0x05EC76F1)
+        uint32_t v = 0x80000000u;
+        for (uint32_t k = 0; k < 8u * threadIdx.x; ++k) v = multmodp(v, 0x05EC76F1u);
+        g_st_x8inv[threadIdx.x] = v;
+    }
+}
+
+struct RotLane {
+    uint32_t lc;       // byte i = (m_i * 32 + r * 4) * 2: the address constant of lookup i (before the >> 1)
+    uint32_t sel[4];   // v_perm selectors of lookups 0..3
+};
+__device__ __forceinline__ RotLane make_rot_lane() {
+    const uint32_t l = lane_id(), r = l & 7u, q = (l >> 3) & 3u;
+    RotLane R;
+    R.lc = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t k = (i + q) & 3u, m = 3u - k;
+        R.lc |= ((m * 32u + r * 4u) * 2u) << (8u * i);
+        R.sel[i] = 0x0C0C0000u | ((4u + k) << 8) | i;
+    }
+    return R;
+}
+
+// One slice-by-4 step: x = crc ^ word, four conflict-free lookups.
+__device__ __forceinline__ uint32_t rot_step(uint32_t x, const RotLane& R, const uint32_t* tab) {
+    uint32_t t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t a = __builtin_amdgcn_perm(x, R.lc, R.sel[i]) >> 1;  // e * 128 + m * 32 + r * 4
+        t[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + a);
+    }
+    return xor3(t[0], t[1], t[2]) ^ t[3];
+}
+
+template <int MODE, int CH>
+__global__ __launch_bounds__(kStThreads) void k_stage(const uint8_t* __restrict__ image, uint64_t nblocks,
+                                                     uint32_t* __restrict__ counts, uint32_t* __restrict__ crcs,
+                                                     unsigned long long* __restrict__ stats) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kTabDw + 4 * kSlotDw];
+    uint32_t* const tab = lds;
+    for (uint32_t d = threadIdx.x; d < kTabDw; d += kStThreads) {
+        const uint32_t e = d >> 5, m = (d >> 3) & 3u;
+        tab[d] = c_tables.t[m][e];
+    }
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t* const slot = lds + kTabDw + wave * kSlotDw;
+    const RotLane R = make_rot_lane();
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kStThreads / 64);
+    unsigned long long c_load = 0, c_walk = 0, c_crc = 0, nblk = 0, nbad = 0, nrec = 0;
+    for (uint64_t b = uint64_t(blockIdx.x) * (kStThreads / 64) + wave; b < nblocks; b += nwaves) {
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        const uint8_t* blk = image + b * kBlockSize;
+        // 1. load: 32 coalesced 1 KiB rows straight into the slot
+#pragma unroll
+        for (uint32_t g = 0; g < 32; ++g)
+            __builtin_amdgcn_global_load_lds(blk + g * 1024u + lane * 16u, slot + g * 256u, 16, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the slot has landed (this wave reads only its own slot)
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        // 2. walk (wave-uniform)
+        const uint32_t bl = kBlockSize;
+        uint32_t offs[4] = {0, 0, 0, 0};
+        uint32_t n = 0, off = 0;
+        if constexpr (MODE & 1) {
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                for (uint32_t j = 0; j < 64u && !done; ++j) {
+                    const uint32_t p = off + 4u;
+                    const uint32_t i0 = p >> 2, i1 = min(i0 + 1u, kSlotDw - 1u);
+                    const uint32_t x = __builtin_amdgcn_alignbyte(slot[i1], slot[i0], p & 3u);
+                    const uint32_t len = x & 0xFFFFu, typ = (x >> 16) & 0xFFu;
+                    if (q < 4) offs[q < 4 ? q : 0] = lane == j ? off : offs[q < 4 ? q : 0];
+                    ++n;
+                    const bool bad = kHeaderSize + len > bl - off || (typ == 0u && len == 0u);
+                    const uint32_t next = off + kHeaderSize + len;
+                    done = bad || bl - next < kHeaderSize;
+                    off = __builtin_amdgcn_readfirstlane(next);
+                }
+                if (q == 4) {  // past 256 records: count only
+                    while (!done) {
+                        const uint32_t p = off + 4u;
+                        const uint32_t i0 = p >> 2, i1 = min(i0 + 1u, kSlotDw - 1u);
+                        const uint32_t x = __builtin_amdgcn_alignbyte(slot[i1], slot[i0], p & 3u);
+                        const uint32_t len = x & 0xFFFFu, typ = (x >> 16) & 0xFFu;
+                        ++n;
+                        const bool bad = kHeaderSize + len > bl - off || (typ == 0u && len == 0u);
+                        const uint32_t next = off + kHeaderSize + len;
+                        done = bad || bl - next < kHeaderSize;
+                        off = __builtin_amdgcn_readfirstlane(next);
+                    }
+                }
+            }
+        }
+        n = __builtin_amdgcn_readfirstlane(n);
+        const uint64_t t2 = __builtin_amdgcn_s_memtime();
+        // 3. checksums: lane k of batch c = record 64 * (CH * c + h) + lane, h < CH
+        if constexpr (MODE & 2) {
+            const uint32_t nl = min(n, 256u);
+#pragma unroll
+            for (int c = 0; c < 4 / CH; ++c) {
+                if (uint32_t(64 * CH * c) >= nl) break;  // wave-uniform
+                uint32_t C[CH], A[CH], sh[CH], nw[CH], lastmask[CH], len[CH], stored[CH], raw0[CH];
+                bool good[CH], has[CH];
+                uint32_t mw = 0;
+#pragma unroll
+                for (int h = 0; h < CH; ++h) {
+                    const uint32_t k = 64u * (CH * c + h) + lane;
+                    has[h] = k < nl;
+                    const uint32_t o = offs[CH * c + h];
+                    const uint32_t a0 = o >> 2;
+                    const uint32_t w0 = slot[a0], w1 = slot[min(a0 + 1u, kSlotDw - 1u)], w2 = slot[min(a0 + 2u, kSlotDw - 1u)];
+                    stored[h] = __builtin_amdgcn_alignbyte(w1, w0, o & 3u);
+                    const uint32_t lt = __builtin_amdgcn_alignbyte(w2, w1, o & 3u);
+                    len[h] = lt & 0xFFFFu;
+                    const uint32_t typ = (lt >> 16) & 0xFFu;
+                    good[h] = has[h] && kHeaderSize + len[h] <= bl - o && !(typ == 0u && len[h] == 0u);
+                    const uint32_t s = o + 6u, nrb = len[h] + 1u;
+                    nw[h] = good[h] ? (nrb + 3u) >> 2 : 0u;
+                    A[h] = s >> 2;
+                    sh[h] = s & 3u;
+                    const uint32_t tail = nrb & 3u;
+                    lastmask[h] = tail ? (1u << (8u * tail)) - 1u : 0xFFFFFFFFu;
+                    C[h] = 0;
+                    raw0[h] = slot[A[h]];
+                    mw = max(mw, nw[h]);
+                }
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) mw = max(mw, (uint32_t)__shfl_xor(mw, m, 64));
+                mw = __builtin_amdgcn_readfirstlane(mw);
+                for (uint32_t k = 0; k < mw; k += 4) {
+                    uint32_t raw[CH][4];
+#pragma unroll
+                    for (int h = 0; h < CH; ++h)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) raw[h][u] = slot[min(A[h] + k + 1u + u, kSlotDw - 1u)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                        for (int h = 0; h < CH; ++h) {
+                            const uint32_t kw = k + u;
+                            uint32_t w = __builtin_amdgcn_alignbyte(raw[h][u], u ? raw[h][u - 1] : raw0[h], sh[h]);
+                            w = kw + 1u == nw[h] ? (w & lastmask[h]) : w;
+                            const uint32_t nc = rot_step(C[h] ^ w, R, tab);
+                            C[h] = kw < nw[h] ? nc : C[h];
+                        }
+                    }
+#pragma unroll
+                    for (int h = 0; h < CH; ++h) raw0[h] = raw[h][3];
+                }
+#pragma unroll
+                for (int h = 0; h < CH; ++h) {
+                    if (has[h]) {
+                        uint32_t crc = 0;
+                        if (good[h]) {
+                            const uint32_t pad = (4u - ((len[h] + 1u) & 3u)) & 3u;
+                            crc = mask(gf_mul(g_st_x8inv[pad], C[h]) ^ g_st_init_xor[len[h] + 1u]);
+                            nbad += crc != stored[h] ? 1u : 0u;
+                        }
+                        crcs[b * 256u + 64u * (CH * c + h) + lane] = crc;
+                        ++nrec;
+                    }
+                }
+            }
+        }
+        const uint64_t t3 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) counts[b] = n;
+        c_load += t1 - t0;
+        c_walk += t2 - t1;
+        c_crc += t3 - t2;
+        ++nblk;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        nbad += __shfl_xor(nbad, m, 64);
+        nrec += __shfl_xor(nrec, m, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&stats[0], c_load);
+        atomicAdd(&stats[1], c_walk);
+        atomicAdd(&stats[2], c_crc);
+        atomicAdd(&stats[3], nblk);
+        atomicAdd(&stats[4], nbad);
+        atomicAdd(&stats[5], nrec);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+int xst_init(void* stream) {
+    hipLaunchKernelGGL(k_st_init, dim3(64), dim3(256), 0, (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// mode: 1 = load + walk, 2 = load + checksums (no walk: offsets 0), 3 = all; ch: 1 or 2 records per lane
+int xst_launch(int mode, int ch, const void* image, uint64_t nblocks, uint32_t* counts, uint32_t* crcs,
+               unsigned long long* stats, int grid, void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const uint8_t* img = static_cast<const uint8_t*>(image);
+#define XST(M, C) hipLaunchKernelGGL((k_stage<M, C>), dim3(grid), dim3(kStThreads), 0, st, img, nblocks, counts, crcs, stats)
+    if (ch == 2) {
+        if (mode == 1) XST(1, 2); else if (mode == 2) XST(2, 2); else XST(3, 2);
+    } else {
+        if (mode == 1) XST(1, 1); else if (mode == 2) XST(2, 1); else if (mode == 0) XST(0, 1); else XST(3, 1);
+    }
+#undef XST
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

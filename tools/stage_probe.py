@@ -1,0 +1,95 @@
+"""Go / no-go probe for VERDICT r5 #1 (tools/experiments/x_stage_probe.hip):
+the small-record verify as one coalesced read per block staged in LDS --
+load, header walk and lane-per-record checksums all from the wave's 32 KiB
+slot.  On bench.py's c3_small image (uniform 64..256-B records, 4 GiB,
+framed on device) it times the probe kernel per mode (HIP events, median of
+5), reads its per-phase shader cycles per block, and checks it: the counts
+equal the production count pass's, and every record's computed CRC equals
+its stored one (a fresh image has no bad record).  The production pipeline
+(count_scan + verify) is timed on the same image for reference.
+
+    make -C tools/experiments xst && python tools/stage_probe.py [--gib 4]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from revel_amd import gpu  # noqa: E402
+from revel_amd._lib import check, lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    X = ctypes.CDLL(os.path.join(ROOT, "tools", "experiments", "libxst.so"))
+    X.xst_init.argtypes = [ctypes.c_void_p]
+    X.xst_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    ctx = gpu.GpuContext(0)
+    st = ctx.stream
+    img, n, nrec = bench.c3_image(ctx, "small", 0x5EED0005, a.gib)
+    nblocks = n // bench.BLOCK_SIZE  # whole blocks only (the probe has no partial-block path)
+    print(f"image {n} B, {nblocks} whole blocks, {nrec} logical records", flush=True)
+    # production reference: counts and time
+    L = lib()
+    counts_ref, first = ctx.alloc(4 * (nblocks + 1)), ctx.alloc(4 * (nblocks + 1))
+    out = ctx.alloc((nrec + 2 * nblocks + 64) * 24)
+    nb_all = (n + 32767) // 32768
+    e0, e1 = ctx.event(), ctx.event()
+    prod = []
+    for _ in range(a.reps):
+        e0.record()
+        check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts_ref.ptr, first.ptr, None))
+        check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, out.ptr, None))
+        e1.record()
+        ctx.sync()
+        prod.append(e0.elapsed_ms(e1))
+    cref = ctx.d2h(counts_ref, 4 * nb_all, np.uint32)[:nblocks]
+    print(f"production count_scan + verify: {np.median(prod):.4f} ms (median of {a.reps})", flush=True)
+    out.free()
+    counts = ctx.alloc(4 * nblocks)
+    crcs = ctx.alloc(4 * 256 * nblocks)
+    stats = ctx.alloc(8 * 8)
+    check(X.xst_init(ctypes.c_void_p(st)))
+    ctx.sync()
+    ncu = 256
+    results = {"image_bytes": n, "blocks": nblocks, "production_ms": float(np.median(prod))}
+    for mode, ch in ((0, 1), (1, 1), (3, 1), (3, 2)):
+        times = []
+        for r in range(a.reps):
+            ctx.memset(stats, 0, 64)
+            e0.record()
+            if X.xst_launch(mode, ch, ctypes.c_void_p(img.ptr), nblocks, ctypes.c_void_p(counts.ptr),
+                            ctypes.c_void_p(crcs.ptr), ctypes.c_void_p(stats.ptr), ncu, ctypes.c_void_p(st)):
+                raise SystemExit("launch failed")
+            e1.record()
+            ctx.sync()
+            times.append(e0.elapsed_ms(e1))
+        s = ctx.d2h(stats, 64, np.uint64)
+        blk = max(1, int(s[3]))
+        row = {"mode": mode, "ch": ch, "ms": round(float(np.median(times)), 4),
+               "cycles_per_block": {"load": round(s[0] / blk), "walk": round(s[1] / blk), "crc": round(s[2] / blk)},
+               "blocks": int(s[3]), "records": int(s[5]), "crc_mismatch": int(s[4])}
+        if mode & 1:
+            cnt = ctx.d2h(counts, 4 * nblocks, np.uint32)
+            row["counts_equal_production"] = bool(np.array_equal(cnt, cref))
+            row["records_expected"] = int(np.minimum(cref, 256).sum())
+        print(json.dumps(row), flush=True)
+        results[f"mode{mode}_ch{ch}"] = row
+    print("RESULT " + json.dumps(results), flush=True)
+
+
+if __name__ == "__main__":
+    main()
