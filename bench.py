@@ -57,8 +57,8 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=None, help="experiment kernel variant (default: production)")
     ap.add_argument("--e2e-gib", type=float, default=None,
                     help="per-rank share of the one-file WAL replayed for the end_to_end field (0 = skip; "
-                         "at most the --blocks image; default min(32, 100 / N): 32 GiB on one GPU, the "
-                         "100 GiB file of BASELINE config C5 from 4 GPUs on)")
+                         "a share larger than the --blocks image repeats it; default 100 / N: the 100 GiB "
+                         "file of BASELINE config C5 at every N)")
     ap.add_argument("--c3-gib", type=float, default=4.0,
                     help="per-rank device-framed Zipf image for the c3 field (0 = skip)")
     ap.add_argument("--c3-small-gib", type=float, default=4.0,
@@ -340,12 +340,28 @@ E2E_CHUNK = 1 << 30  # host bytes per piece of a rank's part (bounds the host co
 
 
 def e2e_share(args, D) -> float:
-    """GiB of the shared WAL file per rank: --e2e-gib, or by default 32 GiB on
-    one GPU and min(32, 100 / N) on N, so the file (and the page cache it
-    fills) stays at C5's 100 GiB instead of growing to 32 N GiB."""
+    """GiB of the shared WAL file per rank: --e2e-gib, or by default 100 / N,
+    so the file is BASELINE config C5's 100 GiB at every N (one GPU replays
+    all of it).  A rank's part repeats its device-resident C2
+    image when the part is larger than the image."""
     if args.e2e_gib is not None:
         return args.e2e_gib
-    return min(32.0, 100.0 / D.world)
+    return 100.0 / D.world
+
+
+def repeat_part(read, img_bytes: int, off: int, m: int) -> np.ndarray:
+    """Bytes [off, off + m) of a rank's part of the end_to_end file: its
+    device image (read(src_offset, nbytes) -> bytes), repeated from byte 0
+    past the image's end.  The image is whole blocks, so every repeat is a
+    valid WAL and the file is C5's size whatever the image's."""
+    out = np.empty(m, np.uint8)
+    done = 0
+    while done < m:
+        src = (off + done) % img_bytes
+        take = min(m - done, img_bytes - src)
+        out[done:done + take] = read(src, take)
+        done += take
+    return out
 
 
 def e2e_write_file(D, per: int, part):
@@ -411,11 +427,12 @@ def end_to_end(ctx, D, dblocks, nblocks: int, gib: float):
     read from the page cache.  `value` times the pipeline (first window read ->
     boundary blob); `all_in_GiB_s` adds the shard's HBM + pinned-ring setup."""
     from revel_amd import shard
-    k = min(nblocks, int(gib * (1 << 30)) // BLOCK_SIZE)
+    k = int(gib * (1 << 30)) // BLOCK_SIZE
     per = k * BLOCK_SIZE
     total = per * D.world
-    # this rank's part of the WAL = its first k device blocks
-    path, why = e2e_write_file(D, per, lambda off, m: ctx.d2h(dblocks, m, src_offset=off))
+    img_bytes = nblocks * BLOCK_SIZE
+    path, why = e2e_write_file(
+        D, per, lambda off, m: repeat_part(lambda src, nb: ctx.d2h(dblocks, nb, src_offset=src), img_bytes, off, m))
     if path is None:
         return {"value": None, "skipped": why}
     D.barrier()
@@ -663,7 +680,7 @@ def main(argv=None):
         progress(D, f"end_to_end: writing and replaying a {e2e_gib:g} GiB-per-rank WAL file")
         e2e = end_to_end(ctx, D, dblocks, n, e2e_gib)
         e2e["sizing"] = ("--e2e-gib" if args.e2e_gib is not None else
-                         "default: min(32, 100 / N) GiB per rank (BASELINE C5's 100 GiB file from 4 GPUs on)")
+                         "default: 100 / N GiB per rank (BASELINE C5's 100 GiB file at every N)")
         progress(D, f"end_to_end: {e2e.get('value')} GiB/s")
 
     c3 = None
@@ -751,7 +768,7 @@ def dry_run(args, D):
     e2e = None
     e2e_gib = e2e_share(args, D)
     if e2e_gib > 0:
-        k = min(args.blocks, int(e2e_gib * (1 << 30)) // BLOCK_SIZE)
+        k = int(e2e_gib * (1 << 30)) // BLOCK_SIZE
         per = k * BLOCK_SIZE
         path, why = e2e_write_file(D, per, lambda off, m: np.zeros(m, np.uint8))
         size = os.path.getsize(path) if path else None

@@ -159,9 +159,9 @@ def test_bench_gpus_8_e2e_skips_together(tmp_path):
 
 
 def test_bench_e2e_share_default_keeps_c5_file_size():
-    """The end_to_end leg's default share: 32 GiB on one GPU,
-    min(32, 100 / N) on N ranks, so the shared file stays at BASELINE C5's
-    100 GiB instead of 32 N GiB; an explicit --e2e-gib wins."""
+    """The end_to_end leg's default share: 100 / N GiB, so the shared file is
+    BASELINE C5's 100 GiB at every N, one GPU included; an
+    explicit --e2e-gib wins."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
@@ -172,9 +172,26 @@ def test_bench_e2e_share_default_keeps_c5_file_size():
 
     dflt = bench.parse([])
     assert dflt.e2e_gib is None
-    assert bench.e2e_share(dflt, _D(1)) == 32.0
-    assert bench.e2e_share(dflt, _D(2)) == 32.0
+    assert bench.e2e_share(dflt, _D(1)) == 100.0
+    assert bench.e2e_share(dflt, _D(2)) == 50.0
     assert bench.e2e_share(dflt, _D(4)) == 25.0
     assert bench.e2e_share(dflt, _D(8)) == 12.5
     assert bench.e2e_share(bench.parse(["--e2e-gib", "0"]), _D(8)) == 0.0
     assert bench.e2e_share(bench.parse(["--e2e-gib", "3"]), _D(8)) == 3.0
+
+
+def test_bench_e2e_part_repeats_the_image():
+    """A rank's part of the end_to_end file larger than its device image
+    repeats the image from byte 0 (whole blocks), piece by piece at any
+    offset, including pieces that straddle the image's end."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+    img = np.arange(5 * 32768, dtype=np.uint64).astype(np.uint8)  # a 5-block stand-in image
+    read = lambda src, nb: img[src:src + nb].copy()  # noqa: E731
+    whole = np.concatenate([img] * 4)
+    for off, m in ((0, 32768), (3 * 32768, 4 * 32768), (5 * 32768 - 7, 20), (100, 15 * 32768 - 200)):
+        got = bench.repeat_part(read, len(img), off, m)
+        assert np.array_equal(got, whole[off:off + m])
