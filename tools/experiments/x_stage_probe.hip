@@ -234,6 +234,73 @@ __global__ __launch_bounds__(kStThreads) void k_stage(const uint8_t* __restrict_
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Scalar-load count pass (probe): the header walk of C blocks per wave on the
+// scalar unit, one s_load of the 12-B header window per hop (SMEM goes to L2
+// through the scalar cache, not the vector L1 whose ~75 misses in flight per
+// CU bound the production count pass).  Counts only; whole blocks and a
+// partial tail alike (the window never reaches past the block).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(4))) const uint64_t cu64;
+template <int C>
+__global__ __launch_bounds__(256) void k_scount(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                               uint32_t* __restrict__ counts) {
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t wg = uint64_t(blockIdx.x) * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = uint64_t(gridDim.x) * 4u;
+    for (uint64_t b0 = wg * C; b0 < nblocks; b0 += nw * C) {
+        uint32_t off[C], n[C], bl[C];
+        bool act[C];
+        const uint8_t* blk[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint64_t b = b0 + c;
+            bl[c] = b < nblocks ? (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - b * kBlockSize) : 0u;
+            act[c] = bl[c] >= 12u;
+            blk[c] = image + (b < nblocks ? b : 0) * kBlockSize;
+            off[c] = 0;
+            n[c] = 0;
+        }
+        // every chain's window load is unconditional (an ended chain re-reads its last one, a
+        // block under 12 bytes reads the image's first 12): the C loads issue back to back and
+        // one lgkmcnt(0) wait covers them all; the updates are selects, no branches
+        const uint8_t* safe[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) safe[c] = bl[c] >= 12u ? blk[c] : image;
+        bool any = true;
+        while (any) {
+            uint64_t w12[C];
+            uint32_t sh[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint32_t a = bl[c] >= 12u ? min(off[c] & ~3u, bl[c] - 12u) : 0u;
+                w12[c] = *(cu64*)(safe[c] + a + 4u);  // header bytes a + 4 .. a + 11: one s_load_dwordx2
+                sh[c] = off[c] - a;
+            }
+            any = false;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint32_t second = (uint32_t)(w12[c] >> (8u * sh[c]));  // bytes off + 4 .. (sh <= 5)
+                const uint32_t len = second & 0xFFFFu, typ = (second >> 16) & 0xFFu;
+                const uint32_t o = off[c];
+                const bool bad = kHeaderSize + len > bl[c] - o || (typ == 0u && len == 0u);
+                const uint32_t next = o + kHeaderSize + len;
+                const bool more = act[c] && !bad && bl[c] - next >= kHeaderSize;
+                n[c] += act[c] ? 1u : 0u;
+                off[c] = more ? next : o;
+                act[c] = more;
+                any = any || more;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint64_t b = b0 + c;
+            if (b < nblocks && lane_id() == 0u) counts[b] = bl[c] >= 12u ? n[c] : (bl[c] >= kHeaderSize ? 1u : 0u);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -253,6 +320,15 @@ int xst_launch(int mode, int ch, const void* image, uint64_t nblocks, uint32_t* 
         if (mode == 1) XST(1, 1); else if (mode == 2) XST(2, 1); else if (mode == 0) XST(0, 1); else XST(3, 1);
     }
 #undef XST
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// scalar-load count pass probe: c = chains per wave (4, 8 or 16), grid workgroups of 4 waves
+int xst_scount(int c, const void* image, uint64_t nbytes, uint32_t* counts, int grid, void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const uint8_t* img = static_cast<const uint8_t*>(image);
+    if (c == 4) hipLaunchKernelGGL(k_scount<4>, dim3(grid), dim3(256), 0, st, img, nbytes, counts);
+    else if (c == 16) hipLaunchKernelGGL(k_scount<16>, dim3(grid), dim3(256), 0, st, img, nbytes, counts);
+    else hipLaunchKernelGGL(k_scount<8>, dim3(grid), dim3(256), 0, st, img, nbytes, counts);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }

@@ -32,7 +32,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--scount", action="store_true",
+                    help="time the scalar-load count pass probe (k_scount) on the small and Zipf images instead")
     a = ap.parse_args()
+    if a.scount:
+        return scount(a)
     X = ctypes.CDLL(os.path.join(ROOT, "tools", "experiments", "libxst.so"))
     X.xst_init.argtypes = [ctypes.c_void_p]
     X.xst_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -89,6 +93,52 @@ def main():
         print(json.dumps(row), flush=True)
         results[f"mode{mode}_ch{ch}"] = row
     print("RESULT " + json.dumps(results), flush=True)
+
+
+def scount(a):
+    """k_scount: the header walk on the scalar unit, C chains per wave, vs the
+    production count pass (k_count_hist) on the same images: counts must be
+    equal, times by HIP events (median of reps)."""
+    X = ctypes.CDLL(os.path.join(ROOT, "tools", "experiments", "libxst.so"))
+    X.xst_scount.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                             ctypes.c_void_p]
+    ctx = gpu.GpuContext(0)
+    st = ctx.stream
+    L = lib()
+    e0, e1 = ctx.event(), ctx.event()
+    res = {}
+    for shape, seed in (("small", 0x5EED0005), ("zipf", 0x5EED0003)):
+        img, n, nrec = bench.c3_image(ctx, shape, seed, a.gib)
+        nb = (n + 32767) // 32768
+        cref, first, cnt = ctx.alloc(4 * nb), ctx.alloc(4 * nb), ctx.alloc(4 * nb)
+        prod = []
+        for _ in range(a.reps):
+            e0.record()
+            check(L.revel_gpu_count_records(ctx.handle, img.ptr, n, cref.ptr, None))
+            e1.record()
+            ctx.sync()
+            prod.append(e0.elapsed_ms(e1))
+        want = ctx.d2h(cref, 4 * nb, np.uint32)
+        row = {"shape": shape, "blocks": nb, "production_count_ms": round(float(np.median(prod)), 4)}
+        for c in (4, 8, 16):
+            for wgs in (8, 16):
+                ts = []
+                for _ in range(a.reps):
+                    ctx.memset(cnt, 0xFF, 4 * nb)
+                    e0.record()
+                    if X.xst_scount(c, ctypes.c_void_p(img.ptr), n, ctypes.c_void_p(cnt.ptr), 256 * wgs,
+                                    ctypes.c_void_p(st)):
+                        raise SystemExit("launch failed")
+                    e1.record()
+                    ctx.sync()
+                    ts.append(e0.elapsed_ms(e1))
+                got = ctx.d2h(cnt, 4 * nb, np.uint32)
+                row[f"c{c}_wg{wgs}"] = {"ms": round(float(np.median(ts)), 4), "counts_equal": bool(np.array_equal(got, want))}
+        print(json.dumps(row), flush=True)
+        res[shape] = row
+        for b in (img, cref, first, cnt):
+            b.free()
+    print("RESULT " + json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
