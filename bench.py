@@ -328,10 +328,26 @@ def c1_reference_path(oracle_c):
             "note": "reference's own reader cannot complete C1 (SURVEY App. A #1-3); LevelDB-correct walk timed"}
 
 
-def e2e_file_path(D) -> tuple:
-    """(directory, path) of the one WAL file every rank of this job shares."""
+def e2e_file_path(D, total: int = 0) -> tuple:
+    """(directory, path) of the one WAL file every rank of this job shares:
+    REVEL_BENCH_DIR when set, else the first of the temp directory and
+    /dev/shm with room for `total` bytes + 1 GiB (C5's 100 GiB file does not
+    fit every box's root file system; it is read from the page cache either
+    way), else the temp directory (the caller's free-space check then skips
+    the leg with its reason).  Every rank computes the same choice before any
+    byte is written (rank 0's truncate allocates nothing)."""
     import tempfile
-    d = os.environ.get("REVEL_BENCH_DIR") or tempfile.gettempdir()
+    d = os.environ.get("REVEL_BENCH_DIR")
+    if not d:
+        cands = [tempfile.gettempdir(), "/dev/shm"]
+        d = cands[0]
+        for c in cands:
+            try:
+                if os.path.isdir(c) and shutil.disk_usage(c).free >= total + (1 << 30):
+                    d = c
+                    break
+            except OSError:
+                continue
     tag = os.environ.get("TORCHELASTIC_RUN_ID") or str(os.getppid() if D.world > 1 else os.getpid())
     return d, os.path.join(d, f"revel_bench_{os.environ.get('MASTER_PORT', 'solo')}_{tag}.log")
 
@@ -372,8 +388,8 @@ def e2e_write_file(D, per: int, part):
     (the headline value is already measured and must still be printed).
     Returns (path, None), or (None, reason) after removing the file.
     REVEL_BENCH_E2E_FAIL_RANK=r makes rank r's write fail (CPU tests)."""
-    d, path = e2e_file_path(D)
     total = per * D.world
+    d, path = e2e_file_path(D, total)
     why = ""
     if D.rank == 0:
         try:
