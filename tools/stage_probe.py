@@ -32,11 +32,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--hybrid", action="store_true",
+                    help="the production count pass over the first blocks beside k_scount over the rest, "
+                         "on two streams at once")
     ap.add_argument("--scount", action="store_true",
                     help="time the scalar-load count pass probe (k_scount) on the small and Zipf images instead")
     a = ap.parse_args()
     if a.scount:
         return scount(a)
+    if a.hybrid:
+        return hybrid(a)
     X = ctypes.CDLL(os.path.join(ROOT, "tools", "experiments", "libxst.so"))
     X.xst_init.argtypes = [ctypes.c_void_p]
     X.xst_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -137,6 +142,59 @@ def scount(a):
         print(json.dumps(row), flush=True)
         res[shape] = row
         for b in (img, cref, first, cnt):
+            b.free()
+    print("RESULT " + json.dumps(res), flush=True)
+
+
+def hybrid(a):
+    """Do the vector and scalar memory paths add up?  The production count
+    pass (vector lanes, revel_gpu_count_records) over blocks [0, nV) on one
+    context's stream and k_scount (scalar unit) over [nV, N) on a second
+    context's stream, launched together; host wall time around both (median
+    of reps), against each alone; the two count arrays together must equal
+    the production pass over the whole image."""
+    import time
+    X = ctypes.CDLL(os.path.join(ROOT, "tools", "experiments", "libxst.so"))
+    X.xst_scount.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                             ctypes.c_void_p]
+    A, B = gpu.GpuContext(0), gpu.GpuContext(0)
+    L = lib()
+    res = {}
+    for shape, seed in (("small", 0x5EED0005), ("zipf", 0x5EED0003)):
+        img, n, nrec = bench.c3_image(A, shape, seed, a.gib)
+        nb = (n + 32767) // 32768
+        cref, cnt = A.alloc(4 * nb), A.alloc(4 * nb)
+        check(L.revel_gpu_count_records(A.handle, img.ptr, n, cref.ptr, None))
+        A.sync()
+        want = A.d2h(cref, 4 * nb, np.uint32)
+        row = {"shape": shape, "blocks": nb}
+
+        def run(nv, vec, sca, c=8, wgs=8):
+            A.sync()
+            B.sync()
+            t0 = time.perf_counter()
+            if vec and nv:
+                check(L.revel_gpu_count_records(A.handle, img.ptr, nv * 32768, cnt.ptr, None))
+            if sca and nv < nb:
+                if X.xst_scount(c, ctypes.c_void_p(img.ptr + nv * 32768), n - nv * 32768,
+                                ctypes.c_void_p(cnt.ptr + 4 * nv), 256 * wgs, ctypes.c_void_p(B.stream)):
+                    raise SystemExit("launch failed")
+            A.sync()
+            B.sync()
+            return (time.perf_counter() - t0) * 1e3
+
+        for f in (0.0, 0.2, 0.3, 0.4):
+            nv = nb - int(f * nb)
+            both = [run(nv, True, True) for _ in range(a.reps + 2)][2:]
+            got = A.d2h(cnt, 4 * nb, np.uint32)
+            vec = [run(nv, True, False) for _ in range(a.reps)]
+            sca = [run(nv, False, True) for _ in range(a.reps)] if f else [0.0]
+            row[f"f{f}"] = {"both_ms": round(float(np.median(both)), 4), "vector_alone_ms": round(float(np.median(vec)), 4),
+                            "scalar_alone_ms": round(float(np.median(sca)), 4),
+                            "counts_equal": bool(np.array_equal(got, want))}
+        print(json.dumps(row), flush=True)
+        res[shape] = row
+        for b in (img, cref, cnt):
             b.free()
     print("RESULT " + json.dumps(res), flush=True)
 
