@@ -174,7 +174,7 @@ def hybrid(a):
             B.sync()
             t0 = time.perf_counter()
             if vec and nv:
-                check(L.revel_gpu_count_records(A.handle, img.ptr, nv * 32768, cnt.ptr, None))
+                check(L.revel_gpu_count_records(A.handle, img.ptr, min(nv * 32768, n), cnt.ptr, None))
             if sca and nv < nb:
                 if X.xst_scount(c, ctypes.c_void_p(img.ptr + nv * 32768), n - nv * 32768,
                                 ctypes.c_void_p(cnt.ptr + 4 * nv), 256 * wgs, ctypes.c_void_p(B.stream)):
