@@ -528,12 +528,14 @@ def c3_image(ctx, shape: str, seed: int, gib: float):
     return img, n, len(sizes)
 
 
-def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: None, stream=None, stream_runs: int = 1):
+def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: None, stream=None, stream_runs: int = 1,
+                    stream_warmup: int = 0):
     """The production verify of a resident image through the C-ABI
     (revel_gpu_count_scan_records -> revel_gpu_verify_records), timed with
     HIP events around both calls, `iters` times, each call isolated (host
     sync after it).  With a list `stream`, then also `iters` calls queued back
-    to back, `stream_runs` times, each run's ms per call appended to it.  Returns (per-iteration ms,
+    to back, `stream_runs` times (after `stream_warmup` untimed calls queued the same
+    way), each run's ms per call appended to it.  Returns (per-iteration ms,
     physical records, records whose status is not OK: the last call's)."""
     from revel_amd._lib import check, lib
     from revel_amd.gpu import RECORD_DTYPE
@@ -561,6 +563,12 @@ def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: Non
         # sample).  The isolated times above also hold the host's submission of
         # the first launch after e0 (~20 us on an idle stream: `gap before`
         # k_count_hist in the traces).
+        # untimed: `stream_warmup` calls queued back to back first, so the
+        # timed runs see the clocks of a sustained load (round 6: without it the
+        # 3 runs fell monotonically, e.g. 0.815 / 0.795 / 0.788 ms on Zipf)
+        for _ in range(stream_warmup):
+            check(L.revel_gpu_count_scan_records(ctx.handle, img.ptr, n, counts.ptr, first.ptr, None))
+            check(L.revel_gpu_verify_records(ctx.handle, img.ptr, n, 0, first.ptr, out.ptr, None))
         for _ in range(stream_runs):
             e0.record()
             for _ in range(iters):
@@ -578,6 +586,9 @@ def c3_verify_timed(ctx, img, n: int, nrec: int, iters: int, barrier=lambda: Non
     return times, nphys, bad
 
 
+C3_STREAM_WARMUP = 27  # ~22 ms of sustained verify before the steady-state runs
+
+
 def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
     """Config C3 on every rank (shape zipf: Zipf(1.1) record sizes 64*k, k in
     [1, 512], seed 0x5EED0003 ^ rank; shape small: 64..256 B, the c3_small
@@ -587,7 +598,8 @@ def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
     seed = (0x5EED0003 if shape == "zipf" else 0x5EED0005) ^ D.rank
     img, n, nrec = c3_image(ctx, shape, seed, gib)
     streamed = []
-    times, nphys, bad = c3_verify_timed(ctx, img, n, nrec, iters, D.barrier, stream=streamed, stream_runs=3)
+    times, nphys, bad = c3_verify_timed(ctx, img, n, nrec, iters, D.barrier, stream=streamed, stream_runs=5,
+                                        stream_warmup=C3_STREAM_WARMUP)
     img.free()
     bad = D.sum(float(bad))
     ms = float(np.median(streamed))
@@ -613,7 +625,7 @@ def c3_records(ctx, D, gib: float, iters: int = 9, shape: str = "zipf"):
             "alg_bytes_per_call": alg,
         },
         "timing": f"median of {len(streamed)} runs of {iters} calls queued back to back between one pair of HIP "
-                  f"events (steady state, ms per call)",
+                  f"events (steady state, ms per call), after {C3_STREAM_WARMUP} untimed calls queued the same way",
         "ms_runs_rank0": [round(x, 4) for x in streamed],
         "spread_pct_rank0": round(100.0 * (max(streamed) - min(streamed)) / ms, 2),
         "ms_isolated": round(iso_max, 4),
