@@ -44,7 +44,10 @@ hipError_t synth_full_blocks(const DeviceInfo& di, void* d_blocks, uint64_t n, u
 // threshold: blocks with more go to k_verify_records_dense.
 constexpr uint32_t kListPerBlock = 64;
 constexpr uint32_t kListCap = 256;
-constexpr uint32_t kListStride = kListCap + 1;
+// kListCap entries + the resume offset, padded to 2 176 B = 17 lines of 128 B:
+// every list starts on a line (the count pass writes them in whole lines)
+constexpr uint32_t kListStride = 272;
+static_assert(kListStride >= kListCap + 1, "a block's list holds kListCap entries and the resume offset");
 hipError_t count_records(const DeviceInfo& di, const void* d_image, uint64_t nbytes, uint32_t* d_counts,
                          uint64_t* d_hlist, hipStream_t st, uint32_t* d_wsums = nullptr);
 // With d_wsums (count_wave_sums(nblocks) u32), the count pass also leaves the

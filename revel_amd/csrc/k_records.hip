@@ -23,71 +23,105 @@ __device__ __forceinline__ Hdr header_in_window(uint3 w, uint32_t sh) {
     return {a, b & 0xFFFFu, (b >> 16) & 0xFFu};
 }
 
-// Per block (one lane each): number of physical records and the first
-// kListCap headers (list_entry; the walk stops at the
-// first bad header, so only the last entry can be bad) followed by the in-block
-// offset of record kListCap when the block has more records.
-// Entries are stored in pairs (below): the pending even entry is flushed on an
-// odd hop or, at the end, for an odd count <= kListCap -- complete only
-// because kListCap is even (entry kListCap - 1 is always the odd one of a pair).
-static_assert(kListCap % 2 == 0, "paired header-list stores need an even kListCap");
-__device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ image, uint64_t nbytes, uint64_t b,
-                                                uint64_t* __restrict__ hlist) {
+// The header walk, one lane per block b = b_wave + lane of a whole wave (lanes
+// past the image walk nothing): each block's number of physical records, and
+// its header list -- the first kListCap headers (list_entry; the walk stops at
+// the first bad header, so only the last entry can be bad), then the in-block
+// offset of record kListCap when the block has more.
+//
+// A hop loads the 12-B window a = min(off & ~3, bl - 12) holding the next
+// header (it never reaches past the block or the image end; off - a <= 5 keeps
+// the 7 header bytes inside it), issued before anything else of the hop: loads
+// and stores share vmcnt, so a store issued first would put its completion
+// into the dependent walk.  The entries go to the wave's LDS slot row n % 16;
+// every kStageHops hops (and at the end) the whole wave writes the group out:
+// lane l stores 16 B (entries 2p, 2p + 1 of the group, p = l % 8) of block
+// 8 i + l / 8, i = 0..7, so a store covers 8 blocks x 128 B -- whole lines,
+// since kListStride keeps every list 128-B aligned -- instead of 64 scattered
+// 16-B pieces every other hop.  Round 6 (profiles/r6/count_*.log, 4 GiB
+// images): without any list stores the walk took 0.57 ms on small records and
+// 34 us on Zipf against 0.93 ms / 48 us with per-lane stores; staged groups of
+// 16 with aligned lists take 0.73 ms / 41 us (8-hop groups: 0.76 ms; unaligned
+// lists: 0.75-0.84 ms).
+constexpr uint32_t kStageHops = 16;
+constexpr uint32_t kStageLanes = kStageHops / 2;     // lanes per block in a group's stores (16 B each)
+constexpr uint32_t kStageBlocks = 64 / kStageLanes;  // blocks per store
+constexpr uint32_t kStageRow = 65;  // u64 per LDS slot row: 64 lanes + 1 (spreads the transposed reads' banks)
+constexpr uint32_t kStageWords = kStageHops * kStageRow;
+static_assert(kListCap % kStageHops == 0, "a group never straddles kListCap");
+static_assert((kListStride * 8u) % 128u == 0, "every block's header list starts on a 128-B line");
+__device__ __forceinline__ uint32_t count_block_wave(const uint8_t* __restrict__ image, uint64_t nbytes,
+                                                     uint64_t b_wave, uint64_t* __restrict__ hlist,
+                                                     uint64_t* __restrict__ stage) {
+    const uint32_t lane = lane_id();
+    const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
+    const uint64_t b = b_wave + lane;
+    const bool inb = b < nblocks;
     const uint64_t base = b * kBlockSize;
-    const uint32_t bl = (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base);
-    const uint8_t* blk = image + base;
+    const uint32_t bl = inb ? (uint32_t)std::min<uint64_t>(kBlockSize, nbytes - base) : 0u;
     uint32_t n = 0;
-    if (bl >= 12u) {
-        // The next header's 12 B are loaded unconditionally, before this
-        // header's list store: loads and stores share vmcnt, so a store
-        // issued first would put its completion into every hop of the
-        // dependent walk.  Window address a = min(off & ~3, bl - 12): a window
-        // never reaches past the block (or the image end), and off - a <= 5
-        // keeps the 7 header bytes inside it.
-        const uint32_t cap = bl - 12u;
-        uint32_t off = 0, a = 0, resume = 0;
-        uint64_t pend = 0;
-        uint64_t* const hl = hlist + b * kListStride;
-        uint3 w = *reinterpret_cast<const uint3*>(blk);
-        for (;;) {
-            const Hdr h = header_in_window(w, off - a);
-            const bool ok = classify(h, off, bl) == REVEL_REC_OK;
-            const uint32_t next = off + kHeaderSize + h.len;  // <= bl when ok
-            const bool more = ok && bl - next >= kHeaderSize;
-            const uint32_t an = min(more ? next & ~3u : 0u, cap);
-            const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
-            // The lanes still walking all stand at the same hop n (they start
-            // together and take one hop per iteration), so n's parity is
-            // wave-uniform: entries are stored in pairs (one 16-B store every
-            // other hop -- the walk is bound by the address unit, TA busy
-            // ~80 %), from record kListCap on the resume offset alone.
-            const uint32_t nu = __builtin_amdgcn_readfirstlane(n);
-            const uint64_t e = list_entry(h);
-            if (nu < kListCap) {
-                if (nu & 1u) {
-                    const uint64_t pair[2] = {pend, e};
-                    __builtin_memcpy(hl + (n - 1u), pair, 16);
-                } else {
-                    pend = e;
-                }
-            } else {
-                resume = n == kListCap ? off : resume;
-                hl[kListCap] = uint64_t(resume);
-            }
-            ++n;
-#ifdef REVEL_COUNT_MAXHOPS  // timing probe only (wrong counts): the walk's tail cost
-            if (n >= REVEL_COUNT_MAXHOPS) break;
-#endif
-            if (!more) break;
-            off = next;
-            a = an;
-            w = wn;
-        }
-        if ((n & 1u) && n <= kListCap) hl[n - 1u] = pend;  // the last entry of an odd count
-    } else if (bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
-        const Hdr h = read_header(blk, 0u, bl);
+    bool walking = bl >= 12u;
+    if (inb && !walking && bl >= kHeaderSize) {  // a last block of 7..11 bytes: one header at most
+        const Hdr h = read_header(image + base, 0u, bl);
         hlist[b * kListStride] = list_entry(h);
         n = 1;
+    }
+    if (!__builtin_amdgcn_ballot_w64(walking)) return n;  // wave-uniform
+    const bool staged = walking;  // (a 7..11-byte block's one entry is stored above)
+    const uint8_t* const blk = image + base;
+    const uint32_t cap = bl - 12u;
+    uint32_t off = 0, a = 0;
+    uint3 w{};
+    if (walking) w = *reinterpret_cast<const uint3*>(blk);
+    // the wave's 64 lists; a store whose offset lies past them is dropped
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        hlist + b_wave * kListStride, (short)0, (int)(64u * kListStride * 8u), 0x00020000);
+    for (uint32_t g0 = 0;; g0 += kStageHops) {  // wave-uniform: a group of kStageHops hops
+        // kStageHops hops for the wave, each lane's masked by its walk: no lane
+        // leaves the loop, so the next window stays in flight in the register
+        // the walk reads it from, across the group's stores
+        for (uint32_t j = 0; j < kStageHops; ++j) {
+            if (walking) {
+                const Hdr h = header_in_window(w, off - a);
+                const bool ok = classify(h, off, bl) == REVEL_REC_OK;
+                const uint32_t next = off + kHeaderSize + h.len;  // <= bl when ok
+                const bool more = ok && bl - next >= kHeaderSize;
+                const uint32_t an = min(more ? next & ~3u : 0u, cap);
+                const uint3 wn = *reinterpret_cast<const uint3*>(blk + an);
+                if (n < kListCap) {
+                    stage[(n % kStageHops) * kStageRow + lane] = list_entry(h);
+                } else if (n == kListCap) {
+                    hlist[b * kListStride + kListCap] = uint64_t(off);  // where record kListCap starts
+                }
+                ++n;
+                walking = more;
+                off = next;
+                a = an;
+                w = wn;
+            }
+        }
+        if (g0 < kListCap) {
+            // every lane: the group out, kStageLanes stores of 8 blocks x 128 B.
+            // Unconditional (a lane with nothing to store points past the
+            // resource): a fixed number of stores, so the compiler's wait for
+            // the next window counts them exactly
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t p = lane % kStageLanes;
+            const uint32_t k = g0 + 2u * p;
+#pragma unroll
+            for (uint32_t i = 0; i < kStageLanes; ++i) {
+                const uint32_t q = kStageBlocks * i + lane / kStageLanes;
+                const uint32_t nq = (uint32_t)__shfl(staged ? min(n, kListCap) : 0u, q, 64);
+                const uint64_t e0 = stage[(2u * p) * kStageRow + q];
+                // (entry k + 1 past the count: a slot no reader takes)
+                const uint64_t e1 = stage[(2u * p + 1u) * kStageRow + q];
+                const u32x4 v = {(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1, (uint32_t)(e1 >> 32)};
+                const uint32_t o = k < nq ? (q * kListStride + k) * 8u : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)o, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!__builtin_amdgcn_ballot_w64(walking)) break;
     }
     return n;
 }
@@ -99,14 +133,12 @@ __device__ __forceinline__ uint32_t count_block(const uint8_t* __restrict__ imag
 __global__ __launch_bounds__(64) void k_count_records(const uint8_t* __restrict__ image, uint64_t nbytes,
                                                       uint32_t* __restrict__ counts, uint64_t* __restrict__ hlist,
                                                       uint32_t* __restrict__ wsums) {
+    __shared__ uint64_t stage[kStageWords];
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
     for (uint64_t b0 = blockIdx.x * 64ull; b0 < nblocks; b0 += gridDim.x * 64ull) {  // wave-uniform
         const uint64_t b = b0 + threadIdx.x;
-        uint32_t n = 0;
-        if (b < nblocks) {
-            n = count_block(image, nbytes, b, hlist);
-            counts[b] = n;
-        }
+        const uint32_t n = count_block_wave(image, nbytes, b0, hlist, stage);
+        if (b < nblocks) counts[b] = n;
         if (wsums) {
             uint32_t t = n;
 #pragma unroll

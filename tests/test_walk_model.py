@@ -5,7 +5,7 @@ per-record CRC): it pins what the GPU kernels compute, independent of a GPU.
 * row_header: the 7 header bytes taken out of a raw 1 KiB row held as 64
   lanes x 16 B (four dwords of lane o >> 4, two more of the next lane or of
   the next row's lane 0 when the type byte lies past the 16 B);
-* the walk over those rows (count_block's rules: a trailer < 7 B ends the
+* the walk over those rows (count_block_wave's rules: a trailer < 7 B ends the
   block, a zero record or a length past the block end ends it, counted);
 * the captures Q_p = P(y_p) x^(8 (S_p - y_p)) (P = zero-init raw CRC of the
   block bytes before y, S = the end of y's 256-B sub-row) at every valid

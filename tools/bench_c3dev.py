@@ -65,7 +65,8 @@ def main():
         if a.walk:
             t, nphys, bad = walk_timed(ctx, img, n, nrec, a.iters)
         else:
-            t, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters, stream=streamed)
+            t, nphys, bad = bench.c3_verify_timed(ctx, img, n, nrec, a.iters, stream=streamed, stream_runs=5,
+                                                      stream_warmup=bench.C3_STREAM_WARMUP)
         times += t
     ms = float(np.median(times))
     mss = float(np.median(streamed)) if streamed else None
