@@ -23,7 +23,7 @@ step 300 "$O/pmc_c2_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$O/c2pmc/pmc1" -o 
 step 300 "$O/pmc_c2_write.log" rocprofv3 --pmc WRITE_SIZE -d "$O/c2pmc/pmc2" -o pmc -f csv -- $C2
 step 60 "$O/pmc_c2_summary.log" python3 "$R/tools/pmc_summary.py" "$O/c2pmc" --json "$R/profiles/pmc_c2.json"
 for shape in zipf small; do
-  L="python3 $R/tools/c3_legs.py --shapes $shape --iters 2"
+  L="python3 $R/tools/c3_legs.py --shapes $shape --iters 2 --warmup-calls 0"
   step 300 "$O/pmc_${shape}_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$O/${shape}pmc/pmc1" -o pmc -f csv -- $L
   step 300 "$O/pmc_${shape}_write.log" rocprofv3 --pmc WRITE_SIZE -d "$O/${shape}pmc/pmc2" -o pmc -f csv -- $L
 done
