@@ -27,6 +27,9 @@ RECORD_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("stored_crc
                          ("computed_crc", "<u4"), ("type", "u1"), ("status", "u1"), ("reserved", "u1", (2,))])
 assert RECORD_DTYPE.itemsize == ctypes.sizeof(RecordResult)
 
+# verify paths of tools/experiments' revel_x_verify_dense_variant
+_DENSE_VARIANTS = {"dense_chunks": 1, "dense_quad": 2, "dense_sorted": 3}
+
 
 def device_count() -> int:
     n = c_int(0)
@@ -193,9 +196,10 @@ class GpuContext:
         small-record kernels, kept in tools/experiments/libexperiments.so
         (not the product): "one_pass" / "one_pass2"
         (the one-pass count + checksum pair revel_x_fused_count_scan ->
-        revel_x_fused_verify), "dense_chunks" / "dense_quad" (the production
-        split with k_verify_dense_chunks or dense2's quad-coalesced loads for
-        the dense blocks); variant: an experiment arm of tools/experiments
+        revel_x_fused_verify), "dense_chunks" / "dense_quad" / "dense_sorted"
+        (the production split with k_verify_dense_chunks, dense2's
+        quad-coalesced loads or round 6's length-sorted batches for the dense
+        blocks); variant: an experiment arm of tools/experiments
         (DESIGN.md 4.2)."""
         if nbytes == 0:
             return np.zeros(0, dtype=RECORD_DTYPE)
@@ -224,10 +228,10 @@ class GpuContext:
             from ._lib import experiments
             check(experiments().revel_x_fused_verify(self._h, image.ptr, nbytes, base_offset, counts.ptr, first.ptr,
                                                      out.ptr, None))
-        elif path in ("dense_chunks", "dense_quad"):
+        elif path in _DENSE_VARIANTS:
             from ._lib import experiments
-            check(experiments().revel_x_verify_dense_variant(self._h, 1 if path == "dense_chunks" else 2, image.ptr,
-                                                             nbytes, base_offset, first.ptr, out.ptr, None))
+            check(experiments().revel_x_verify_dense_variant(self._h, _DENSE_VARIANTS[path], image.ptr, nbytes,
+                                                             base_offset, first.ptr, out.ptr, None))
         elif path is not None:
             check(L.revel_gpu_verify_records_path(self._h, path, image.ptr, nbytes, base_offset, first.ptr, out.ptr,
                                                   None))

@@ -86,11 +86,11 @@ def test_walk_pipeline_vs_oracle(gpu_ctx, golden_index):
 # ---- round 5's small-record kernels (moved out of the product in round 6) ----
 # "one_pass" / "one_pass2": the one-pass count + checksum pair
 # (revel_x_fused_count_scan mode 1 / 2 -> revel_x_fused_verify);
-# "dense_chunks" / "dense_quad": the production split with
-# k_verify_dense_chunks or dense2's quad-coalesced loads for the dense blocks
-# (revel_x_verify_dense_variant).  Every verify test of test_gpu.py that the
+# "dense_chunks" / "dense_quad" / "dense_sorted": the production split with
+# k_verify_dense_chunks, dense2's quad-coalesced loads or round 6's
+# length-sorted batches for the dense blocks (revel_x_verify_dense_variant).  Every verify test of test_gpu.py that the
 # product runs over its VERIFY_PATHS runs here over these.
-EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad"]
+EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad", "dense_sorted"]
 
 
 @pytest.fixture

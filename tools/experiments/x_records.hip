@@ -26,6 +26,7 @@ namespace {
 #include "x_verify_chunks.inc"
 #include "x_verify_fused2.inc"
 #include "x_verify_dense_quad.inc"
+#include "x_verify_dense_sorted.inc"
 
 // Header-list entries past kListCap of the blocks the one-pass kernels left
 // (fb[0] counts them; none: the launch leaves at once).
@@ -464,7 +465,7 @@ hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbyt
 hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* img, uint64_t nbytes,
                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                 const uint64_t* hl, const uint32_t* d_counts, bool list_ready, hipStream_t st) {
-    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 2) return hipErrorInvalidValue;
+    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 3) return hipErrorInvalidValue;
     hipError_t e = ensure_len_tables(di, st);
     if (e != hipSuccess) return e;
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
@@ -498,9 +499,12 @@ hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* 
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_verify_records_dense2<kListCap, true>), dim3(grid), dim3(kDenseThreads), 0, st, img,
                            nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole);
-    } else {
+    } else if (dense == 2) {
         hipLaunchKernelGGL((k_verify_records_dense2q<>), dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
                            base_offset, d_first, d_out, hl, d_counts, dense_whole);
+    } else {
+        hipLaunchKernelGGL(k_verify_records_dense3, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
+                           d_first, d_out, hl, d_counts, dense_whole);
     }
     return hipGetLastError();
 }
@@ -570,7 +574,8 @@ extern "C" __attribute__((visibility("default"))) int revel_x_fused_verify(
 }
 
 // The production split with another dense kernel (1: k_verify_dense_chunks +
-// dense2 over the rest; 2: dense2 with quad-coalesced loads), after
+// dense2 over the rest; 2: dense2 with quad-coalesced loads; 3: dense2 with
+// length-sorted batches, x_verify_dense_sorted.inc), after
 // revel_gpu_count_scan_records of the same image on this context (its header
 // lists and block order).
 extern "C" __attribute__((visibility("default"))) int revel_x_verify_dense_variant(
