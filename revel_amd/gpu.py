@@ -28,7 +28,9 @@ RECORD_DTYPE = np.dtype([("file_offset", "<u8"), ("length", "<u4"), ("stored_crc
 assert RECORD_DTYPE.itemsize == ctypes.sizeof(RecordResult)
 
 # verify paths of tools/experiments' revel_x_verify_dense_variant
-_DENSE_VARIANTS = {"dense_chunks": 1, "dense_quad": 2, "dense_sorted": 3}
+_DENSE_VARIANTS = {"dense_chunks": 1, "dense_quad": 2, "dense_sorted": 3, "dense_staged": 5,
+                   "dense_staged_1ch": 4, "dense_staged_12w": 7, "dense_staged_12w_1ch": 6,
+                   "dense_staged_a16": 12, "dense_staged_a16_8w": 13}
 
 
 def device_count() -> int:

@@ -9,7 +9,7 @@ import pytest
 import test_gpu
 from conftest import golden_image
 from oracle import oracle_c as oc
-from test_gpu import compare_walk, kat_blocks, run_full, zipf_image
+from test_gpu import BLOCK_SIZE, compare_walk, kat_blocks, run_full, zipf_image
 
 # Not part of the driver's `-m gpu` product suite: run with `-m experiment` on
 # a GPU box after `make -C tools/experiments` (conftest skips them otherwise).
@@ -88,9 +88,13 @@ def test_walk_pipeline_vs_oracle(gpu_ctx, golden_index):
 # (revel_x_fused_count_scan mode 1 / 2 -> revel_x_fused_verify);
 # "dense_chunks" / "dense_quad" / "dense_sorted": the production split with
 # k_verify_dense_chunks, dense2's quad-coalesced loads or round 6's
-# length-sorted batches for the dense blocks (revel_x_verify_dense_variant).  Every verify test of test_gpu.py that the
-# product runs over its VERIFY_PATHS runs here over these.
-EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad", "dense_sorted"]
+# length-sorted batches for the dense blocks (revel_x_verify_dense_variant);
+# "dense_staged*": round 6's batch spans staged in LDS (8 or 12 waves per CU,
+# 2 or 1 chains per lane, x_verify_dense_staged.inc).  Every verify test of
+# test_gpu.py that the product runs over its VERIFY_PATHS runs here over these.
+STAGED_PATHS = ["dense_staged", "dense_staged_1ch", "dense_staged_12w", "dense_staged_12w_1ch", "dense_staged_a16",
+                "dense_staged_a16_8w"]
+EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad", "dense_sorted"] + STAGED_PATHS
 
 
 @pytest.fixture
@@ -158,3 +162,44 @@ def test_exp_256_records_then_bad_header(gpu_ctx, path, ending):
     assert len(ref) == n + 1 and ref["status"][n] != 0
     dimg = gpu_ctx.upload(np.frombuffer(img, dtype=np.uint8))
     compare_walk(gpu_ctx.verify_image(dimg, len(img), path=path), ref)
+
+
+LONG_SHAPES = ["long_last", "long_first", "long_mid_flip", "over_256", "two_long", "tail"]
+
+
+@pytest.mark.parametrize("path", STAGED_PATHS + [None])
+@pytest.mark.parametrize("shape", LONG_SHAPES)
+def test_exp_dense_blocks_with_long_records(gpu_ctx, path, shape):
+    """Dense blocks (more than 64 records) that also hold a record longer
+    than a staged batch's LDS slot (8-16 KiB): the staged kernels checksum it
+    piece by piece with the whole wave; checked field by field against the
+    oracle walk, with flips inside the long records and next to them."""
+    rng = np.random.default_rng(LONG_SHAPES.index(shape))
+    tiny = lambda k: [rng.integers(0, 256, int(rng.integers(0, 24)), dtype=np.uint8).tobytes() for _ in range(k)]
+    big = lambda n: rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    recs = []
+    for blk in range(6):
+        if shape == "long_last":
+            recs += tiny(90) + [big(BLOCK_SIZE - 90 * 20 - 200 - int(rng.integers(0, 300)))]
+        elif shape == "long_first":
+            recs += [big(20000 + int(rng.integers(0, 5000)))] + tiny(120)
+        elif shape == "long_mid_flip":
+            recs += tiny(70) + [big(12000 + 997 * blk)] + tiny(100)
+        elif shape == "over_256":
+            recs += [b""] * 300 + [big(16000 + int(rng.integers(0, 9000)))] + tiny(10)
+        elif shape == "two_long":
+            recs += tiny(66) + [big(9000 + 13 * blk), big(8190 + 111 * blk)] + tiny(40)
+        else:
+            recs += tiny(200) + [big(13000)]
+    img = bytearray(oc.write_image(recs))
+    ref = oc.walk(bytes(img))
+    for v in range(3, len(ref), 29):
+        if int(ref["length"][v]) > 0:
+            off = int(ref["file_offset"][v]) + 7 + int(rng.integers(0, int(ref["length"][v])))
+            img[off] ^= 1 << int(rng.integers(0, 8))
+    if shape == "tail":
+        img = img[:len(img) - 777]  # a partial dense last block
+    ref = oc.walk(bytes(img))
+    assert (np.bincount(ref["file_offset"] // BLOCK_SIZE) > 64).any()
+    dimg = gpu_ctx.upload(np.frombuffer(bytes(img), dtype=np.uint8))
+    test_gpu.compare_walk(gpu_ctx.verify_image(dimg, len(img), path=path), ref)

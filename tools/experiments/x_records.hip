@@ -27,6 +27,7 @@ namespace {
 #include "x_verify_fused2.inc"
 #include "x_verify_dense_quad.inc"
 #include "x_verify_dense_sorted.inc"
+#include "x_verify_dense_staged.inc"
 
 // Header-list entries past kListCap of the blocks the one-pass kernels left
 // (fb[0] counts them; none: the launch leaves at once).
@@ -465,7 +466,7 @@ hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbyt
 hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* img, uint64_t nbytes,
                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                 const uint64_t* hl, const uint32_t* d_counts, bool list_ready, hipStream_t st) {
-    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 3) return hipErrorInvalidValue;
+    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 15) return hipErrorInvalidValue;
     hipError_t e = ensure_len_tables(di, st);
     if (e != hipSuccess) return e;
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
@@ -502,9 +503,29 @@ hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* 
     } else if (dense == 2) {
         hipLaunchKernelGGL((k_verify_records_dense2q<>), dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes,
                            base_offset, d_first, d_out, hl, d_counts, dense_whole);
-    } else {
+    } else if (dense == 3) {
         hipLaunchKernelGGL(k_verify_records_dense3, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
                            d_first, d_out, hl, d_counts, dense_whole);
+    } else {
+        // 4..7: batch spans staged in LDS (x_verify_dense_staged.inc): 8 or 12 waves per CU, 1 or 2 chains per lane
+        // (8..11: timing probes of 6 and 4, wrong results: loads only / checksums only)
+#define XSG(NW, CH, P, ...)                                                                                             \
+    hipLaunchKernelGGL((k_verify_records_dense4<NW, CH, P, ##__VA_ARGS__>), dim3(grid_for(di, nblocks, NW)),            \
+                       dim3(SgCfg<NW>::threads), 0, st, img, nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole)
+        if (dense == 4) XSG(8, 1, 0);
+        else if (dense == 5) XSG(8, 2, 0);
+        else if (dense == 6) XSG(12, 1, 0);
+        else if (dense == 7) XSG(12, 2, 0);
+        else if (dense == 8) XSG(12, 1, 1);
+        else if (dense == 9) XSG(12, 1, 2);
+        else if (dense == 10) XSG(8, 1, 1);
+        else if (dense == 11) XSG(8, 1, 2);
+        // 12..15: aligned groups read by ds_read_b128 (sg_crc16); 14 / 15 timing probes (checksums only)
+        else if (dense == 12) XSG(12, 1, 0, true);
+        else if (dense == 13) XSG(8, 1, 0, true);
+        else if (dense == 14) XSG(12, 1, 2, true);
+        else XSG(8, 1, 2, true);
+#undef XSG
     }
     return hipGetLastError();
 }
@@ -575,7 +596,8 @@ extern "C" __attribute__((visibility("default"))) int revel_x_fused_verify(
 
 // The production split with another dense kernel (1: k_verify_dense_chunks +
 // dense2 over the rest; 2: dense2 with quad-coalesced loads; 3: dense2 with
-// length-sorted batches, x_verify_dense_sorted.inc), after
+// length-sorted batches, x_verify_dense_sorted.inc; 4..7: batch spans staged in LDS,
+// x_verify_dense_staged.inc), after
 // revel_gpu_count_scan_records of the same image on this context (its header
 // lists and block order).
 extern "C" __attribute__((visibility("default"))) int revel_x_verify_dense_variant(
