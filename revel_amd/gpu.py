@@ -30,7 +30,7 @@ assert RECORD_DTYPE.itemsize == ctypes.sizeof(RecordResult)
 # verify paths of tools/experiments' revel_x_verify_dense_variant
 _DENSE_VARIANTS = {"dense_chunks": 1, "dense_quad": 2, "dense_sorted": 3, "dense_staged": 5,
                    "dense_staged_1ch": 4, "dense_staged_12w": 7, "dense_staged_12w_1ch": 6,
-                   "dense_staged_a16": 12, "dense_staged_a16_8w": 13}
+                   "dense_staged_a16": 12, "dense_staged_a16_8w": 13, "dense_pairs": 16}
 
 
 def device_count() -> int:

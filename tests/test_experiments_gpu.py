@@ -94,7 +94,7 @@ def test_walk_pipeline_vs_oracle(gpu_ctx, golden_index):
 # test_gpu.py that the product runs over its VERIFY_PATHS runs here over these.
 STAGED_PATHS = ["dense_staged", "dense_staged_1ch", "dense_staged_12w", "dense_staged_12w_1ch", "dense_staged_a16",
                 "dense_staged_a16_8w"]
-EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad", "dense_sorted"] + STAGED_PATHS
+EXPERIMENT_PATHS = ["one_pass", "one_pass2", "dense_chunks", "dense_quad", "dense_sorted", "dense_pairs"] + STAGED_PATHS
 
 
 @pytest.fixture
@@ -167,7 +167,7 @@ def test_exp_256_records_then_bad_header(gpu_ctx, path, ending):
 LONG_SHAPES = ["long_last", "long_first", "long_mid_flip", "over_256", "two_long", "tail"]
 
 
-@pytest.mark.parametrize("path", STAGED_PATHS + [None])
+@pytest.mark.parametrize("path", STAGED_PATHS + ["dense_pairs", None])
 @pytest.mark.parametrize("shape", LONG_SHAPES)
 def test_exp_dense_blocks_with_long_records(gpu_ctx, path, shape):
     """Dense blocks (more than 64 records) that also hold a record longer

@@ -28,6 +28,7 @@ namespace {
 #include "x_verify_dense_quad.inc"
 #include "x_verify_dense_sorted.inc"
 #include "x_verify_dense_staged.inc"
+#include "x_verify_dense_pairs.inc"
 
 // Header-list entries past kListCap of the blocks the one-pass kernels left
 // (fb[0] counts them; none: the launch leaves at once).
@@ -466,7 +467,7 @@ hipError_t fused_verify(const DeviceInfo& di, const void* d_image, uint64_t nbyt
 hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* img, uint64_t nbytes,
                                 uint64_t base_offset, const uint32_t* d_first, revel_record_result* d_out,
                                 const uint64_t* hl, const uint32_t* d_counts, bool list_ready, hipStream_t st) {
-    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 15) return hipErrorInvalidValue;
+    if (!aligned16(img) || !hl || !d_counts || dense < 1 || dense > 16) return hipErrorInvalidValue;
     hipError_t e = ensure_len_tables(di, st);
     if (e != hipSuccess) return e;
     const uint64_t nblocks = (nbytes + kBlockSize - 1) / kBlockSize;
@@ -506,6 +507,10 @@ hipError_t verify_dense_variant(const DeviceInfo& di, int dense, const uint8_t* 
     } else if (dense == 3) {
         hipLaunchKernelGGL(k_verify_records_dense3, dim3(grid), dim3(kDenseThreads), 0, st, img, nbytes, base_offset,
                            d_first, d_out, hl, d_counts, dense_whole);
+    } else if (dense == 16) {
+        // lane pairs on whole lines (x_verify_dense_pairs.inc)
+        hipLaunchKernelGGL(k_verify_records_dense5, dim3(grid_for(di, nblocks, kPairThreads / 64)), dim3(kPairThreads),
+                           0, st, img, nbytes, base_offset, d_first, d_out, hl, d_counts, dense_whole);
     } else {
         // 4..7: batch spans staged in LDS (x_verify_dense_staged.inc): 8 or 12 waves per CU, 1 or 2 chains per lane
         // (8..11: timing probes of 6 and 4, wrong results: loads only / checksums only)
