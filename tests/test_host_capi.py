@@ -32,6 +32,25 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
 
 
+def test_integration_rust_binding_matches_header():
+    """INTEGRATION.md's Rust extern blocks (section 2 + 2b) declare every
+    function of include/revel_wal.h exactly once, with the header's argument
+    count (the binding a Revel maintainer would compile)."""
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
+        doc = f.read()
+    rust = dict(re.findall(r"pub fn (revel_\w+)\s*\(([^)]*)\)", doc))
+    names = re.findall(r"pub fn (revel_\w+)\s*\(", doc)
+    assert len(names) == len(set(names)), "a function is bound twice"
+    with open(os.path.join(ROOT, "include", "revel_wal.h")) as f:
+        text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    protos = dict(re.findall(r"\b(revel_[a-z0-9_]+)\s*\(([^;{)]*(?:\([^)]*\)[^;{)]*)*)\)\s*;", text))
+    assert set(rust) == set(protos), set(rust) ^ set(protos)
+    for name, cargs in protos.items():
+        n_c = 0 if cargs.strip() in ("", "void") else cargs.count(",") + 1
+        n_r = 0 if not rust[name].strip() else rust[name].count(",") + 1
+        assert n_c == n_r, (name, cargs, rust[name])
+
+
 def test_gpu_entry_points_fail_loudly_without_device():
     if gpu.device_count() > 0:
         pytest.skip("a GPU is visible")
