@@ -1,11 +1,15 @@
 // host_io.h -- host-side helpers shared by the replay paths (replay.cpp,
-// shard.cpp): NUMA placement next to a GPU and parallel window fills.
+// shard.cpp): NUMA placement next to a GPU, parallel window fills and the
+// release of consumed file-mapping ranges.
 #pragma once
 #include <ctype.h>
 #include <hip/hip_runtime_api.h>
 #include <sched.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -80,6 +84,18 @@ class NodeBinding {
     cpu_set_t saved_;
     bool active_ = false;
 };
+
+// Drop the page-table entries of the whole pages inside [p, p + n) of a
+// read-only file mapping once a fill thread has copied them out (the pages
+// stay in the page cache; a later access would fault them back in).  A window
+// at a time, on the fill threads beside the PCIe-bound copy, instead of one
+// munmap of the whole mapping at the end: for C5's 100 GiB file that final
+// teardown took ~1.1 s of the call on the GPU box (~26 M PTEs), 32 of 51 GiB/s.
+inline void release_mapped(const void* p, uint64_t n) {
+    static const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = ((uintptr_t)p + pg - 1) & ~(pg - 1), b = ((uintptr_t)p + n) & ~(pg - 1);
+    if (b > a) (void)::madvise(reinterpret_cast<void*>(a), b - a, MADV_DONTNEED);
+}
 
 // Fill dst[0..len) from the source with up to `threads` parallel workers.
 template <typename F>

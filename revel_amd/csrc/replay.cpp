@@ -231,7 +231,10 @@ int revel_gpu_replay_file(revel_gpu_context* ctx, const char* path, uint64_t off
         if (m) (void)::madvise(m, length, MADV_SEQUENTIAL);
         const uint8_t* src = static_cast<const uint8_t*>(m);
         rc = replay(ctx, length, offset, mode, window_bytes, nbuffers, io_threads, out,
-                    [&](uint8_t* dst, uint64_t rel, uint64_t n) { memcpy(dst, src + rel, n); });
+                    [&](uint8_t* dst, uint64_t rel, uint64_t n) {
+                        memcpy(dst, src + rel, n);
+                        revel::release_mapped(src + rel, n);  // the final munmap then has little to tear down
+                    });
         if (m) ::munmap(m, length);
     } else {
         const uint64_t align = io == REVEL_REPLAY_IO_DIRECT ? 4096 : 1;

@@ -259,7 +259,9 @@ void blob_write(const Boundary& B, uint8_t* q) {
 }
 
 // Load + verify (+ reassemble) shard bytes src[0, length) = WAL [offset, +length).
-int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int io_threads) {
+// release_src: src is the library's own mapping of the WAL file, whose
+// consumed windows the fill threads release (host_io.h release_mapped).
+int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int io_threads, bool release_src) {
     revel_gpu_context* ctx = s->ctx;
     revel_wal_shard_info& I = s->info;
     revel::DeviceGuard guard(ctx->di.device);
@@ -305,6 +307,7 @@ int shard_load(revel_wal_shard* s, const uint8_t* src, size_t window_bytes, int 
             uint8_t* h = R.h[slot];
             I.read_seconds += revel::parallel_fill(threads, len, [&](uint64_t o, uint64_t n) {
                 memcpy(h + o, src + off + o, n);
+                if (release_src) revel::release_mapped(src + off + o, n);
             });
             TRY(hipEventRecord(R.e0[slot], R.copy), "hipEventRecord");
             TRY(hipMemcpyAsync(static_cast<uint8_t*>(s->d_image) + off, h, len, hipMemcpyHostToDevice, R.copy),
@@ -603,7 +606,7 @@ int revel_gpu_wal_shard_load(revel_gpu_context* ctx, const char* path, const uin
     revel_wal_shard* s = nullptr;
     int rc = new_shard(ctx, file_bytes, offset, length, checksum, flags, &s);
     if (rc) return rc;
-    rc = shard_load(s, src ? src + offset : nullptr, window_bytes, io_threads);
+    rc = shard_load(s, src ? src + offset : nullptr, window_bytes, io_threads, path != nullptr);
     if (rc) {
         delete s;
         return rc;
@@ -784,7 +787,7 @@ int revel_gpu_replay_sharded(revel_gpu_context* const* ctxs, int n, const char* 
     std::vector<std::thread> pool;
     for (int k = 0; k < n; ++k)
         pool.emplace_back([&, k] {
-            rcs[k] = shard_load(R->shards[k], src ? src + offs[k] : nullptr, window_bytes, io_threads);
+            rcs[k] = shard_load(R->shards[k], src ? src + offs[k] : nullptr, window_bytes, io_threads, path != nullptr);
             if (rcs[k]) msgs[k] = revel_last_error();
         });
     for (auto& t : pool) t.join();
